@@ -1,0 +1,345 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors under tests/golden/ by running the REFERENCE modules.
+
+Runs only in the build container (it reads /root/reference, which does not exist on
+the GPU box).  The reference's own torch modules produce every expected output here:
+
+  sgmse.backbones.ncsnpp.NCSNpp            (ncsnpp.py:36-404)
+  sgmse.backbones.ncsnpp_utils.layerspp     (ResnetBlockBigGANpp 214-276, AttnBlockpp 64-93,
+                                             GaussianFourierProjection 32-43)
+  sgmse.backbones.ncsnpp_utils.up_or_down_sampling (upsample_2d/downsample_2d 195-257)
+  sgmse.backbones.snrnet.SNRNet             (snrnet.py:47-97)
+  sgmse.sdes.{OUVESDE,BBED}                 (sdes.py:149-307)
+  sgmse.sampling.get_pc_sampler             (sampling/__init__.py:28-80)
+
+Import recipe: stub torch.utils.cpp_extension.load before importing, so
+the op/ package does not JIT-compile CUDA; the CPU paths never touch the stub.
+
+Modules that do not import here (sgmse.model / data_module need pytorch_lightning,
+torchaudio) are restated from source text for the STFT / transform / preconditioning
+glue, citing the lines.  Inputs and injected noise come from snrse.formula so the tests
+can regenerate them instead of storing them.  Only outputs are stored.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+import wave
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference/sgmse-bbed"
+OUT = os.path.join(REPO, "tests", "golden")
+
+sys.path.insert(0, os.path.join(REPO, "snr-aligned_diffse_amd"))
+from snrse import formula  # noqa: E402
+
+os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
+sys.dont_write_bytecode = True
+import torch.utils.cpp_extension as _ce  # noqa: E402
+
+_ce.load = lambda *a, **k: None
+sys.path.insert(0, REF)
+from sgmse.backbones import BackboneRegistry  # noqa: E402
+from sgmse.backbones.ncsnpp_utils import layerspp, up_or_down_sampling  # noqa: E402
+from sgmse.backbones.snrnet import SNRNet  # noqa: E402
+from sgmse import sdes as ref_sdes  # noqa: E402
+from sgmse import sampling as ref_sampling  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def load_formula(module: torch.nn.Module, prefix: str = ""):
+    sd = module.state_dict()
+    shapes = {prefix + k: tuple(v.shape) for k, v in sd.items()}
+    vals = formula.formula_state_dict(shapes)
+    module.load_state_dict({k: torch.from_numpy(vals[prefix + k]) for k in sd})
+    return module
+
+
+def fnormal(name, shape, complex_=False):
+    return torch.from_numpy(formula.normal_tensor(name, shape, complex_))
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrays.items()})
+    print(f"wrote {path} ({os.path.getsize(path)} B)")
+
+
+def t2n(x):
+    return x.detach().cpu().numpy()
+
+
+# ---------------------------------------------------------------------------------
+def gen_keys():
+    net = BackboneRegistry.get_by_name("ncsnpp")()
+    keys = [[k, list(v.shape)] for k, v in net.state_dict().items()]
+    frozen = [n for n, p in net.named_parameters() if not p.requires_grad]
+    trainable_order = [n for n, p in net.named_parameters() if p.requires_grad]
+    snr = SNRNet()
+    skeys = [[k, list(v.shape)] for k, v in snr.state_dict().items()]
+    with open(os.path.join(OUT, "state_dict_keys.json"), "w") as f:
+        json.dump({"ncsnpp": keys, "ncsnpp_frozen": frozen,
+                   "ncsnpp_trainable_order": trainable_order, "snrnet": skeys}, f)
+    print("wrote state_dict_keys.json", len(keys), len(skeys))
+
+
+def gen_fir():
+    x = fnormal("golden.fir.x", (2, 8, 16, 32))
+    k = [1, 3, 3, 1]
+    up = up_or_down_sampling.upsample_2d(x, k, factor=2)
+    dn = up_or_down_sampling.downsample_2d(x, k, factor=2)
+    save("fir.npz", up=t2n(up), down=t2n(dn))
+
+
+def gen_blocks():
+    act = torch.nn.SiLU()
+    out = {}
+    cfgs = {
+        "plain": dict(in_ch=128, out_ch=128, up=False, down=False, hw=(8, 16)),
+        "cin_ne_cout": dict(in_ch=128, out_ch=256, up=False, down=False, hw=(8, 8)),
+        "down": dict(in_ch=128, out_ch=128, up=False, down=True, hw=(8, 16)),
+        "up": dict(in_ch=256, out_ch=256, up=True, down=False, hw=(4, 8)),
+        "cat384": dict(in_ch=384, out_ch=256, up=False, down=False, hw=(4, 8)),
+    }
+    for name, c in cfgs.items():
+        rb = layerspp.ResnetBlockBigGANpp(act=act, in_ch=c["in_ch"], out_ch=c["out_ch"],
+                                          temb_dim=512, up=c["up"], down=c["down"],
+                                          dropout=0.0, fir=True, fir_kernel=[1, 3, 3, 1],
+                                          skip_rescale=True, init_scale=0.0).eval()
+        load_formula(rb, f"rb_{name}.")
+        x = fnormal(f"golden.rb_{name}.x", (2, c["in_ch"]) + c["hw"])
+        temb = fnormal(f"golden.rb_{name}.temb", (2, 512))
+        with torch.no_grad():
+            y = rb(x, temb)
+            gn = act(rb.GroupNorm_0(x))
+        out[f"{name}_out"] = t2n(y)
+        if name == "plain":
+            out[f"{name}_gn0silu"] = t2n(gn)
+    save("resblocks.npz", **out)
+
+
+def gen_attn():
+    blk = layerspp.AttnBlockpp(channels=256, skip_rescale=True, init_scale=0.0).eval()
+    load_formula(blk, "attn.")
+    x = fnormal("golden.attn.x", (2, 256, 16, 8))
+    with torch.no_grad():
+        y = blk(x)
+    save("attn.npz", out=t2n(y))
+
+
+def gen_ncsnpp():
+    net = BackboneRegistry.get_by_name("ncsnpp")().eval()
+    load_formula(net)
+    x = fnormal("golden.ncsnpp.x", (2, 2, 256, 64), complex_=True) * 0.5
+    t = torch.tensor([0.5, 0.8], dtype=torch.float32)
+    with torch.no_grad():
+        # temb path pieces (ncsnpp.py:256-275)
+        m = net.all_modules
+        temb = m[0](torch.log(t))
+        temb = m[2](torch.nn.functional.silu(m[1](temb)))
+        y = net(x, t)
+    save("ncsnpp_full.npz", out=t2n(y), temb=t2n(temb), t=t2n(t))
+
+
+def gen_sde():
+    ts = torch.tensor([0.03, 0.2, 0.5, 0.8, 0.999], dtype=torch.float32)
+    ou = ref_sdes.OUVESDE(theta=1.5, sigma_min=0.05, sigma_max=0.5, N=30)
+    ou1 = ref_sdes.OUVESDE(theta=1.5, sigma_min=0.05, sigma_max=1.0, N=30)
+    bb = ref_sdes.BBED(T_sampling=0.999, k=2.6, theta=0.52, N=30)
+    x = fnormal("golden.sde.x", (5, 1, 4, 4), complex_=True)
+    y = fnormal("golden.sde.y", (5, 1, 4, 4), complex_=True)
+    out = {"t": t2n(ts)}
+    for nm, s in (("ouve", ou), ("ouve_smax1", ou1), ("bbed", bb)):
+        d, g = s.sde(x, ts[:, None, None, None], y)
+        out[f"{nm}_drift"] = t2n(d)
+        out[f"{nm}_g"] = t2n(torch.as_tensor(g)).reshape(-1)
+        out[f"{nm}_std"] = t2n(s._std(ts)).astype(np.float64)
+        out[f"{nm}_mean"] = t2n(s._mean(x, ts, y))
+    save("sde.npz", **out)
+
+
+class _NoiseTape:
+    """Monkeypatches torch.randn_like so the reference sampler consumes formula noise
+    (draw i is normal_tensor(f"{tag}.{i}") with torch's complex convention)."""
+
+    def __init__(self, tag):
+        self.tag, self.i, self._orig = tag, 0, None
+
+    def __enter__(self):
+        self._orig = torch.randn_like
+
+        def fake(x, *a, **k):
+            z = fnormal(f"{self.tag}.{self.i}", tuple(x.shape), complex_=torch.is_complex(x))
+            self.i += 1
+            return z.to(x.dtype) if not torch.is_complex(x) else z.to(x.dtype)
+
+        torch.randn_like = fake
+        return self
+
+    def __exit__(self, *exc):
+        torch.randn_like = self._orig
+
+
+def gen_pc_ouve():
+    net = BackboneRegistry.get_by_name("ncsnpp")().eval()
+    load_formula(net)
+    Y = fnormal("golden.pc.Y", (2, 1, 256, 64), complex_=True) * 0.5
+    sde = ref_sdes.OUVESDE(theta=1.5, sigma_min=0.05, sigma_max=0.5, N=5)
+
+    def score_fn(x, t, y):  # ScoreModel.forward, model_type='bbed' (model.py:485-489)
+        return -net(torch.cat([x, y], dim=1), t)
+
+    sampler = ref_sampling.get_pc_sampler("reverse_diffusion", "ald", sde=sde, score_fn=score_fn,
+                                          Y=Y, eps=0.03, snr=0.5, corrector_steps=1)
+    with torch.no_grad(), _NoiseTape("golden.pc.noise") as tape:
+        xr, ns = sampler()
+    save("pc_ouve.npz", out=t2n(xr), ns=np.int64(ns), draws=np.int64(tape.i))
+
+
+def gen_pc_variants():
+    """Sampler arithmetic with a cheap analytic score (no network): every predictor /
+    corrector pairing, OUVE and BBED, so the SDE/PC kernels are pinned independently."""
+    Y = fnormal("golden.pcv.Y", (2, 1, 16, 8), complex_=True)
+
+    def score_fn(x, t, y):
+        return -(x - y) * 0.7 + 0.1 * y
+
+    out = {}
+    # 'euler_maruyama' is not pinned: the reference's pc loop passes `stepsize` as a 4th
+    # positional argument that EulerMaruyamaPredictor forwards into sde.sde() -> TypeError
+    # (sampling/__init__.py:72, predictors.py:46-49, sdes.py:192).
+    cases = [("ouve", "reverse_diffusion", "ald"), ("ouve", "reverse_diffusion", "langevin"),
+             ("ouve", "reverse_diffusion", "none"), ("ouve", "none", "ald"),
+             ("bbed", "reverse_diffusion", "ald")]
+    for sde_name, pred, corr in cases:
+        if sde_name == "ouve":
+            sde = ref_sdes.OUVESDE(theta=1.5, sigma_min=0.05, sigma_max=0.5, N=6)
+            Yc = Y
+        else:  # BBED works only for B=1 in the reference (sdes.py:276), see DESIGN.md
+            sde = ref_sdes.BBED(T_sampling=0.999, k=2.6, theta=0.52, N=6)
+            Yc = Y[:1]
+        sampler = ref_sampling.get_pc_sampler(pred, corr, sde=sde, score_fn=score_fn, Y=Yc,
+                                              eps=0.03, snr=0.5, corrector_steps=1)
+        tag = f"golden.pcv.{sde_name}.{pred}.{corr}"
+        with torch.no_grad(), _NoiseTape(tag) as tape:
+            xr, ns = sampler()
+        key = f"{sde_name}__{pred}__{corr}"
+        out[key] = t2n(xr).astype(np.complex128)
+        out[key + "__ns"] = np.int64(ns)
+        out[key + "__draws"] = np.int64(tape.i)
+    save("pc_variants.npz", **out)
+
+
+def read_wav(path):
+    with wave.open(path) as w:
+        assert w.getsampwidth() == 2 and w.getnchannels() == 1
+        raw = np.frombuffer(w.readframes(w.getnframes()), dtype="<i2")
+    return raw.copy()
+
+
+def stft_ref(sig):  # SpecsDataModule.stft: data_module.py:269-278, 291-293 (window 13-19)
+    win = torch.hann_window(510, periodic=True)
+    return torch.stft(sig, n_fft=510, hop_length=128, window=win, center=True, return_complex=True)
+
+
+def istft_ref(spec, length):  # data_module.py:295-297
+    win = torch.hann_window(510, periodic=True)
+    return torch.istft(spec, n_fft=510, hop_length=128, window=win, center=True, length=length)
+
+
+def spec_fwd_ref(spec):  # data_module.py:241-254, exponent 0.5, factor 0.15
+    return spec.abs() ** 0.5 * torch.exp(1j * spec.angle()) * 0.15
+
+
+def spec_back_ref(spec):  # data_module.py:256-267
+    spec = spec / 0.15
+    return spec.abs() ** (1 / 0.5) * torch.exp(1j * spec.angle())
+
+
+def pad_spec_ref(Y, m=64):  # util/other.py:83-99
+    T = Y.size(3)
+    n = (m - T % m) if T % m else 0
+    return torch.nn.functional.pad(Y, (0, n, 0, 0))
+
+
+def gen_stft():
+    base = "/root/reference/dataset/VBD_SNR-5/valid2"
+    noisy = read_wav(f"{base}/noisy/p232_001.wav")
+    clean = read_wav(f"{base}/clean/p232_001.wav")
+    y = torch.from_numpy(noisy.astype(np.float32) / 32768.0)[None]  # torchaudio.load scaling
+    nf = y.abs().max()
+    Y = stft_ref(y / nf)
+    Yf = spec_fwd_ref(Y)
+    back = istft_ref(spec_back_ref(Yf), y.shape[1])
+    # istft of a network-sized (T padded to 64) spectrogram, as to_audio does (model.py:612-613)
+    Ypad = pad_spec_ref(Yf[:, None])[:, 0]
+    Ypad = Ypad + 0.01 * fnormal("golden.stft.pert", tuple(Ypad.shape), complex_=True)
+    wav_pad = istft_ref(spec_back_ref(Ypad[0]), y.shape[1])
+    save("stft.npz", noisy_i16=noisy, clean_i16=clean, stft=t2n(Y), spec_fwd=t2n(Yf),
+         roundtrip=t2n(back), istft_padded=t2n(wav_pad))
+
+
+def gen_snrnet():
+    net = SNRNet().eval()
+    load_formula(net, "snrnet.")
+    x = fnormal("golden.snrnet.x", (2, 2, 256, 64))
+    with torch.no_grad():
+        y = net(x)
+    save("snrnet.npz", out=t2n(y))
+
+
+T_30 = (0.001 ** (1 / 7) + (np.arange(1, 31) - 1) / 29 * (1 - 0.001 ** (1 / 7))) ** 7  # model.py:22-23
+
+
+def gen_sebridge_enhance():
+    """ScoreModel.enhance, model_type='sebridge_v3', snr_conditioned='true', oracle SNR
+    (model.py:702-839), restated glue around the reference NCSNpp module."""
+    net = BackboneRegistry.get_by_name("ncsnpp")().eval()
+    load_formula(net)
+    base = "/root/reference/dataset/VBD_SNR-5/valid"
+    noisy = read_wav(f"{base}/noisy/p232_001.wav")
+    with open(f"{base}/active_rms.txt") as f:
+        _, clean_rms, noise_rms = f.readline().split("\t")
+    clean_rms, noise_rms = float(clean_rms), float(noise_rms)
+    fixed_snr, sigma_max = 0.17783, 0.5
+    y = torch.from_numpy(noisy.astype(np.float32) / 32768.0)[None]
+    T_orig = y.size(1)
+    est_snr = torch.FloatTensor([noise_rms / clean_rms])  # model.py:722-724
+    norm_factor = y.abs().max().item()
+    t_ = (est_snr / (10 ** 0.25 * fixed_snr)).numpy()  # calculate_snr_direct 627-629
+    t_ = T_30[np.abs(T_30 - t_).argmin()]
+    est_snr_ = torch.FloatTensor([10 ** 0.25 * fixed_snr * t_])
+    normfac_ = (2.040166) * (0.240253 + 0.759747 * fixed_snr ** 2) ** 0.5 / ((1 + est_snr_ ** 2) ** 0.5)
+    norm_factor = norm_factor * normfac_
+    y = y / norm_factor
+    Y = pad_spec_ref(torch.unsqueeze(spec_fwd_ref(stft_ref(y)), 0))
+    vec_t = torch.ones(1, 1, 1, 1) * float(t_)
+    Z = fnormal("golden.enh.Z", tuple(Y.shape), complex_=True) * sigma_max * float(t_)
+    X_T = Y + Z
+    eps, sd = 0.001, 0.5  # sebridge_v3 preconditioning, model.py:536-541
+    c_skip = sd ** 2 / ((vec_t - eps) ** 2 + sd ** 2)
+    c_out = (sd * (vec_t - eps)) / ((sd ** 2 + vec_t ** 2) ** 0.5)
+    with torch.no_grad():
+        sample = c_skip * X_T + c_out * net(torch.cat([X_T, Y], dim=1), vec_t.reshape(1))
+        x_hat = istft_ref(spec_back_ref(sample.squeeze()), T_orig) * norm_factor
+    save("enhance_sebridge.npz", x_hat=t2n(x_hat).reshape(-1), t_hat=np.float64(t_),
+         norm_factor=t2n(norm_factor).reshape(-1), score=t2n(sample))
+
+
+if __name__ == "__main__":
+    os.makedirs(OUT, exist_ok=True)
+    which = sys.argv[1:] or ["keys", "fir", "blocks", "attn", "ncsnpp", "sde", "pc_ouve",
+                             "pc_variants", "stft", "snrnet", "sebridge"]
+    table = {"keys": gen_keys, "fir": gen_fir, "blocks": gen_blocks, "attn": gen_attn,
+             "ncsnpp": gen_ncsnpp, "sde": gen_sde, "pc_ouve": gen_pc_ouve,
+             "pc_variants": gen_pc_variants, "stft": gen_stft, "snrnet": gen_snrnet,
+             "sebridge": gen_sebridge_enhance}
+    for w in which:
+        torch.manual_seed(0)
+        table[w]()
