@@ -1,0 +1,123 @@
+/* snrse.h — C-ABI of libsnrse_hip.so, the MI355X (gfx950) kernels of the
+ * reverse-diffusion speech-enhancement path of yh-jun/SNR-Aligned_diffSE
+ * (ScoreModel.enhance() / PC sampler, sgmse-bbed/sgmse/model.py:702-839).
+ *
+ * Conventions
+ *   - Plain pointers to DEVICE memory, sizes as int, a hipStream_t (NULL = legacy stream);
+ *     every launch is stream-ordered and asynchronous, nothing is allocated inside except
+ *     where a caller-provided workspace is named.  Entries are reentrant per stream.
+ *   - Return 0 on success or a hipError_t code (hipErrorInvalidValue = 1 for a bad
+ *     argument); snrse_error_string() maps it to text.  The Python host maps non-zero to
+ *     RuntimeError, as the reference's TORCH_CHECK does (op/upfirdn2d.cpp:8-19).
+ *   - dtype: SNRSE_F32 = 0 (exact fp32 "parity" mode), SNRSE_BF16 = 1 (bf16 storage,
+ *     fp32 accumulation).  Activations are NHWC: [B, F(=H), T(=W), C].
+ *   - Complex spectrograms are interleaved complex64 [B, F, T] (= the reference's
+ *     [B, 1, F, T] tensors).
+ */
+#ifndef SNRSE_H_
+#define SNRSE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* hipStream_t;
+
+enum { SNRSE_F32 = 0, SNRSE_BF16 = 1 };
+
+int snrse_abi_version(void);
+const char* snrse_error_string(int code);
+int snrse_device_name(char* buf, int len);
+
+/* Generic FIR resampling on [major, in_h, in_w, minor] — replaces the reference's only
+ * native op binding, upfirdn2d(input, kernel, up_x, up_y, down_x, down_y, pad_x0, pad_x1,
+ * pad_y0, pad_y1) (op/upfirdn2d.cpp:12-23, op/upfirdn2d_kernel.cu:209-369, semantics of
+ * upfirdn2d_native op/upfirdn2d.py:159-200).  `kernel` is [kh, kw] f32 on the device;
+ * `out` is caller-allocated [major, out_h, out_w, minor] with
+ * out_h = (in_h*up_y + pad_y0 + pad_y1 - kh)/down_y + 1 (out_w likewise). */
+int snrse_upfirdn2d(const void* in, void* out, const float* kernel, int major, int in_h, int in_w,
+                    int minor, int kh, int kw, int up_x, int up_y, int down_x, int down_y,
+                    int pad_x0, int pad_x1, int pad_y0, int pad_y1, int dtype, hipStream_t stream);
+
+/* Implicit-GEMM convolution (3x3 pad 1 or 1x1), stride 1, NHWC, on MFMA.
+ * Replaces ddpm_conv3x3 / ddpm_conv1x1 / NIN (ncsnpp_utils/layers.py:100-124, 546-555).
+ *   input channels = concat(src0 [.., C0], src1 [.., C1]) (torch.cat, ncsnpp.py:337)
+ *   wgt    [Npad][ksize*ksize*(C0+C1)] packed (Cout, ky, kx, Cin), dtype; Npad = Cout
+ *          rounded up to 128 (Cout >= 64) or 16 (Cout <= 16, zero rows)
+ *   sc_src/sc_src1 (optional): 1x1 shortcut input(s) appended as extra K; sc_wgt [Npad][Csc+Csc1]
+ *   out[m][n] = ((acc + bias[n] + temb[b][n] + res[m][n]) * out_scale)
+ *               + (comb_src ? comb_src[m][0:4] . comb_w[n][0:4] + comb_b[n] : 0)
+ *   out_f32: write float output (bf16 mode pyramid heads); res then is float too. */
+int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, int B, int H, int W, int ksize,
+                 const void* wgt, const void* sc_src, int Csc, const void* sc_src1, int Csc1,
+                 const void* sc_wgt, const float* bias, const float* temb, int temb_stride,
+                 const void* res, int res_ld, float out_scale, const float* comb_src,
+                 const float* comb_w, const float* comb_b, void* out, int Cout, int out_ld,
+                 int dtype, int out_f32, hipStream_t stream);
+
+/* GroupNorm statistics (nn.GroupNorm, layerspp.py:221,233): per-channel (sum, sumsq) of
+ * concat(src0, src1) over H*W into sums [B][C0+C1][2] (double; zeroed by the call). */
+int snrse_gn_stats(const void* src0, int C0, const void* src1, int C1, int B, int HW, double* sums,
+                   int dtype, hipStream_t stream);
+
+/* Fused GroupNorm-apply (+SiLU) (+FIR [1,3,3,1] down/up x2) (layerspp.py:245-257,
+ * up_or_down_sampling.py:195-257).  sums == NULL: identity normalisation (plain FIR of x).
+ * mode: 0 none, 1 down (out H/2 x W/2), 2 up (out 2H x 2W).  out [B][Ho][Wo][C0+C1]. */
+int snrse_gn_apply(const void* src0, int C0, const void* src1, int C1, int B, int H, int W,
+                   const double* sums, const float* gamma, const float* beta, int groups, float eps,
+                   int act, int mode, void* out, int dtype, hipStream_t stream);
+
+/* AttnBlockpp attention core (layerspp.py:84-88): qkv [B][L][3C] -> out [B][L][C],
+ * softmax(q k^T / sqrt(C)) v, flash-style on MFMA.  C must be 256. */
+int snrse_attention(const void* qkv, void* out, int B, int L, int C, int dtype, hipStream_t stream);
+
+/* Time embedding (ncsnpp.py:256-275): temb[b] = W2 silu(W1 [sin, cos](2 pi log t W_gfp) + b1) + b2. */
+int snrse_temb_mlp(const float* t, const float* Wg, const float* W1, const float* b1, const float* W2,
+                   const float* b2, float* temb, int B, int nf, hipStream_t stream);
+/* All ResBlock Dense_0 projections (layerspp.py:264-265): out[b][r] = W[r] . silu(temb[b]) + bias[r]. */
+int snrse_temb_dense(const float* temb, const float* W, const float* bias, float* out, int B, int R, int D,
+                     hipStream_t stream);
+
+/* Network input (ncsnpp.py:253-254, 282-285): complex x, y [B,F,T] -> im2col [B,F,T,64]
+ * (tap-major 3x3 x {x.re, x.im, y.re, y.im}, zero padded) in dtype, and the f32 input
+ * pyramid [B,F,T,4]. */
+int snrse_input_pack(const void* x, const void* y, int B, int H, int W, void* col, float* pyr, int dtype,
+                     hipStream_t stream);
+
+/* Output head + preconditioning + SDE step (ncsnpp.py:398-404, model.py:481-541,
+ * predictors.py:75-80, correctors.py:69-81).  pyr [B,F,T,4] (f32 if pyr_f32 else bf16),
+ * t [B], score_mode 0 = -dnn ('bbed'), 1 = c_skip x + c_out dnn ('sebridge*').
+ * coef [B][4] = {a, by, c, s}: x_mean = a x + by y + c score; x_out = x_mean + s z.
+ * z = noise (complex64 tensor) or, if noise == NULL, Philox4x32-10(seed, offset + index)
+ * complex normal with each part N(0, 1/2).  x_out == NULL: only score_out is written. */
+int snrse_score_update(const void* pyr, int pyr_f32, const float* out_w, const float* out_b,
+                       const float* t, int score_mode, int B, int HW, const void* x, const void* y,
+                       const void* noise, uint64_t seed, uint64_t offset, const float* coef,
+                       void* x_out, void* xmean_out, void* score_out, hipStream_t stream);
+
+/* Same step for an arbitrary score tensor (generic score_fn). */
+int snrse_sde_update(const void* x, const void* y, const void* score, const void* noise, uint64_t seed,
+                     uint64_t offset, const float* coef, int B, int HW, void* x_out, void* xmean_out,
+                     hipStream_t stream);
+
+/* out = coef[b][0] x + coef[b][1] y + coef[b][3] z (prior sampling, sdes.py:225-232, 298-304). */
+int snrse_axpby_noise(const void* x, const void* y, const void* noise, uint64_t seed, uint64_t offset,
+                      const float* coef, int B, int HW, void* out, hipStream_t stream);
+
+/* STFT (data_module.py:291-293 with spec_fwd 241-254 and pad_spec other.py:83-90):
+ * sig [B][L] f32 -> out complex64 [B][256][Tpad], frames 1 + L/128 (the rest zero).
+ * mode 0 raw, 1 exponent transform (|X|^0.5 e^{i angle X} * 0.15).  in_scale multiplies sig. */
+int snrse_stft(const float* sig, int B, int L, float in_scale, int Tpad, int mode, void* out,
+               hipStream_t stream);
+
+/* iSTFT (data_module.py:295-297 with spec_back 256-267): spec complex64 [B][256][T] -> out [B][L]
+ * f32, times out_scale[b] (NULL = 1).  frames: workspace of B*T*510 floats. */
+int snrse_istft(const void* spec, int B, int T, int L, int mode, const float* out_scale, float* frames,
+                float* out, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SNRSE_H_ */

@@ -1,0 +1,68 @@
+// Shared device helpers for the snrse HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SNRSE_DEV __device__ __forceinline__
+
+// Element storage types.  bf16 is kept as raw 16-bit patterns so loads/stores stay
+// vectorised (Guideline 13) and conversions are explicit.
+typedef uint16_t bf16_t;
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_mfma;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+SNRSE_DEV float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// round-to-nearest-even f32 -> bf16 (NaN kept a NaN)
+SNRSE_DEV bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static constexpr int kBytes = 4;
+  SNRSE_DEV static float to_f(float v) { return v; }
+  SNRSE_DEV static float from_f(float v) { return v; }
+};
+template <> struct Elem<bf16_t> {
+  static constexpr int kBytes = 2;
+  SNRSE_DEV static float to_f(bf16_t v) { return bf2f(v); }
+  SNRSE_DEV static bf16_t from_f(float v) { return f2bf(v); }
+};
+
+SNRSE_DEV float silu(float x) { return x / (1.0f + __expf(-x)); }
+
+// Accurate SiLU for the fp32 parity mode (matches torch's x * sigmoid(x) to ~1 ulp).
+SNRSE_DEV float silu_exact(float x) { return x / (1.0f + expf(-x)); }
+
+SNRSE_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+SNRSE_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+SNRSE_DEV double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// dtype codes shared with the C-ABI (include/snrse.h)
+enum { SNRSE_F32 = 0, SNRSE_BF16 = 1 };
+
+#define SNRSE_RET(expr)                              \
+  do {                                               \
+    hipError_t _e = (expr);                          \
+    if (_e != hipSuccess) return (int)_e;            \
+  } while (0)
+#define SNRSE_LAUNCH_CHECK() SNRSE_RET(hipGetLastError())
+#define SNRSE_EINVAL ((int)hipErrorInvalidValue)

@@ -1,0 +1,284 @@
+// Network front/back kernels of the score model and the SDE predictor/corrector update.
+//
+//   snrse_temb_mlp     GaussianFourierProjection(log t) -> Linear -> SiLU -> Linear
+//                      (layerspp.py:32-43, ncsnpp.py:256-275); one block per utterance.
+//   snrse_temb_dense   all 49 ResBlock Dense_0(SiLU(temb)) projections in one launch
+//                      (layerspp.py:264-265), weights concatenated on the host.
+//   snrse_input_pack   complex (x, y) -> 4 real channels (ncsnpp.py:253-254), unrolled over
+//                      the 3x3 taps of the input conv (im2col, 36 of 64 channels used) so the
+//                      first conv (ncsnpp.py:285) is a K=64 GEMM on MFMA; also writes the
+//                      4-channel input pyramid (ncsnpp.py:282) in f32.
+//   snrse_score_update output head + preconditioning + one SDE step, fused:
+//                      dnn = output_layer(pyr / t) as complex (ncsnpp.py:398-404),
+//                      score = -dnn (model_type 'bbed', model.py:488-489) or
+//                      c_skip x + c_out dnn (sebridge*, model.py:536-541),
+//                      x_mean = a x + by y + c score,  x = x_mean + s z  with z complex
+//                      normal (each part N(0,1/2), torch.randn_like on complex64), which covers
+//                      ReverseDiffusionPredictor (predictors.py:75-80), AnnealedLangevinDynamics
+//                      (correctors.py:69-81) and EulerMaruyamaPredictor (predictors.py:46-52).
+//                      z is read from a tensor (parity mode) or drawn in-kernel (Philox4x32-10).
+#include "common.h"
+
+namespace {
+
+constexpr float kTwoPi = 6.28318530717958647692f;
+
+__global__ __launch_bounds__(512) void temb_mlp_kernel(const float* t, const float* Wg, const float* W1,
+                                                       const float* b1, const float* W2, const float* b2,
+                                                       float* temb, int nf) {
+  // nf = 128: e[256], h[512], out[512]
+  __shared__ float e[256];
+  __shared__ float h[512];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float lt = logf(t[b]);
+  if (tid < nf) {
+    const float pr = lt * Wg[tid] * kTwoPi;
+    e[tid] = sinf(pr);
+    e[nf + tid] = cosf(pr);
+  }
+  __syncthreads();
+  {
+    float acc = b1[tid];
+    const float* w = W1 + (size_t)tid * 2 * nf;
+    for (int k = 0; k < 2 * nf; ++k) acc = fmaf(w[k], e[k], acc);
+    h[tid] = silu_exact(acc);
+  }
+  __syncthreads();
+  {
+    float acc = b2[tid];
+    const float* w = W2 + (size_t)tid * 4 * nf;
+    for (int k = 0; k < 4 * nf; ++k) acc = fmaf(w[k], h[k], acc);
+    temb[(size_t)b * 4 * nf + tid] = acc;
+  }
+}
+
+// out[b][r] = W[r] . silu(temb[b]) + bias[r];  block: 256 threads = 4 waves, 16 rows per wave
+__global__ __launch_bounds__(256) void temb_dense_kernel(const float* temb, const float* W, const float* bias,
+                                                         float* out, int B, int R, int D) {
+  extern __shared__ float st[];  // [B][D] silu(temb)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int i = tid; i < B * D; i += 256) st[i] = silu_exact(temb[i]);
+  __syncthreads();
+  const int r0 = blockIdx.x * 64 + wid * 16;
+  for (int rr = 0; rr < 16; ++rr) {
+    const int r = r0 + rr;
+    if (r >= R) break;
+    const float* w = W + (size_t)r * D;
+    float wv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wv[i] = (lane + 64 * i < D) ? w[lane + 64 * i] : 0.f;
+    for (int b = 0; b < B; ++b) {
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (lane + 64 * i < D) acc = fmaf(wv[i], st[b * D + lane + 64 * i], acc);
+      acc = wave_sum(acc);
+      if (lane == 0) out[(size_t)b * R + r] = acc + bias[r];
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void input_pack_kernel(const float2* x, const float2* y, int H, int W,
+                                                         T* col, float* pyr, int total) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= total) return;
+  const int HW = H * W;
+  const int b = p / HW, rem = p - b * HW, h = rem / W, w = rem - (rem / W) * W;
+  const float2 xv = x[p], yv = y[p];
+  float4 pv = make_float4(xv.x, xv.y, yv.x, yv.y);
+  *(float4*)(pyr + (size_t)p * 4) = pv;
+  T* dst = col + (size_t)p * 64;
+  float v[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) v[i] = 0.f;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
+    if (hh < 0 || hh >= H || ww < 0 || ww >= W) continue;
+    const size_t q = (size_t)b * HW + (size_t)hh * W + ww;
+    const float2 a = x[q], c = y[q];
+    v[tap * 4 + 0] = a.x; v[tap * 4 + 1] = a.y; v[tap * 4 + 2] = c.x; v[tap * 4 + 3] = c.y;
+  }
+#pragma unroll
+  for (int i = 0; i < 64; ++i) dst[i] = Elem<T>::from_f(v[i]);
+}
+
+// ---- Philox4x32-10 -> Box-Muller complex normals -------------------------------------
+SNRSE_DEV uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t& hi) {
+  const uint64_t p = (uint64_t)a * b;
+  hi = (uint32_t)(p >> 32);
+  return (uint32_t)p;
+}
+SNRSE_DEV u32x4 philox(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0, hi1;
+    const uint32_t lo0 = mulhilo(0xD2511F53u, c[0], hi0);
+    const uint32_t lo1 = mulhilo(0xCD9E8D57u, c[2], hi1);
+    c = u32x4{hi1 ^ c[1] ^ k0, lo1, hi0 ^ c[3] ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+SNRSE_DEV float u01(uint32_t v) { return ((v >> 8) + 0.5f) * (1.0f / 16777216.0f); }  // (0,1)
+
+SNRSE_DEV float2 cnormal(uint64_t seed, uint64_t ctr) {
+  const u32x4 r = philox(u32x4{(uint32_t)ctr, (uint32_t)(ctr >> 32), 0x5eedu, 0u}, (uint32_t)seed,
+                         (uint32_t)(seed >> 32));
+  const float rad = sqrtf(-2.0f * logf(u01(r[0])));
+  float sn, cs;
+  sincosf(kTwoPi * u01(r[1]), &sn, &cs);
+  // complex normal with E|z|^2 = 1: each part N(0, 1/2)
+  return make_float2(rad * cs * 0.70710678118654752f, rad * sn * 0.70710678118654752f);
+}
+
+struct StepCoef {
+  float a, by, c, s;  // x_mean = a x + by y + c score ; x = x_mean + s z
+};
+
+template <typename TP>
+__global__ __launch_bounds__(256) void score_update_kernel(
+    const TP* pyr, const float* out_w, const float* out_b, const float* t, int score_mode, int HW, int total,
+    const float2* x, const float2* y, const float2* noise, uint64_t seed, uint64_t offset, const float* coef,
+    float2* x_out, float2* xmean_out, float2* score_out) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= total) return;
+  const int b = p / HW;
+  const float tb = t[b];
+  const float inv_t = 1.0f / tb;
+  float h[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) h[i] = Elem<TP>::to_f(pyr[(size_t)p * 4 + i]) * inv_t;
+  float dre = out_b[0], dim = out_b[1];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    dre = fmaf(out_w[i], h[i], dre);
+    dim = fmaf(out_w[4 + i], h[i], dim);
+  }
+  const float2 xv = x[p];
+  float2 sc;
+  if (score_mode == 0) {  // bbed: score = -dnn
+    sc = make_float2(-dre, -dim);
+  } else {  // sebridge preconditioning, eps = 0.001, sigma_data = 0.5
+    const float te = tb - 0.001f;
+    const float c_skip = 0.25f / (te * te + 0.25f);
+    const float c_out = (0.5f * te) / sqrtf(0.25f + tb * tb);
+    sc = make_float2(c_skip * xv.x + c_out * dre, c_skip * xv.y + c_out * dim);
+  }
+  if (score_out) score_out[p] = sc;
+  if (!x_out) return;
+  const float* cf = coef + 4 * b;
+  const float2 yv = y ? y[p] : make_float2(0.f, 0.f);
+  float2 xm;
+  xm.x = cf[0] * xv.x + cf[1] * yv.x + cf[2] * sc.x;
+  xm.y = cf[0] * xv.y + cf[1] * yv.y + cf[2] * sc.y;
+  if (xmean_out) xmean_out[p] = xm;
+  float2 z = noise ? noise[p] : cnormal(seed, offset + (uint64_t)p);
+  x_out[p] = make_float2(xm.x + cf[3] * z.x, xm.y + cf[3] * z.y);
+}
+
+// x = a x + by y + s z (prior sampling, sdes.py:225-232 / 298-304)
+__global__ __launch_bounds__(256) void axpby_noise_kernel(const float2* x, const float2* y, const float2* noise,
+                                                          uint64_t seed, uint64_t offset, const float* coef,
+                                                          int HW, int total, float2* out) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= total) return;
+  const float* cf = coef + 4 * (p / HW);
+  const float2 xv = x ? x[p] : make_float2(0.f, 0.f);
+  const float2 yv = y ? y[p] : make_float2(0.f, 0.f);
+  const float2 z = noise ? noise[p] : cnormal(seed, offset + (uint64_t)p);
+  out[p] = make_float2(cf[0] * xv.x + cf[1] * yv.x + cf[3] * z.x, cf[0] * xv.y + cf[1] * yv.y + cf[3] * z.y);
+}
+
+// generic step for an arbitrary score tensor: x_mean = a x + by y + c score; x = x_mean + s z
+__global__ __launch_bounds__(256) void sde_update_kernel(const float2* x, const float2* y, const float2* score,
+                                                         const float2* noise, uint64_t seed, uint64_t offset,
+                                                         const float* coef, int HW, int total, float2* x_out,
+                                                         float2* xmean_out) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= total) return;
+  const float* cf = coef + 4 * (p / HW);
+  const float2 xv = x[p];
+  const float2 yv = y ? y[p] : make_float2(0.f, 0.f);
+  const float2 sc = score ? score[p] : make_float2(0.f, 0.f);
+  float2 xm;
+  xm.x = cf[0] * xv.x + cf[1] * yv.x + cf[2] * sc.x;
+  xm.y = cf[0] * xv.y + cf[1] * yv.y + cf[2] * sc.y;
+  if (xmean_out) xmean_out[p] = xm;
+  const float2 z = noise ? noise[p] : cnormal(seed, offset + (uint64_t)p);
+  x_out[p] = make_float2(xm.x + cf[3] * z.x, xm.y + cf[3] * z.y);
+}
+
+}  // namespace
+
+extern "C" int snrse_sde_update(const void* x, const void* y, const void* score, const void* noise, uint64_t seed,
+                                uint64_t offset, const float* coef, int B, int HW, void* x_out, void* xmean_out,
+                                hipStream_t s) {
+  const int total = B * HW;
+  if (total <= 0 || !x || !coef || !x_out) return SNRSE_EINVAL;
+  hipLaunchKernelGGL(sde_update_kernel, dim3((total + 255) / 256), dim3(256), 0, s, (const float2*)x,
+                     (const float2*)y, (const float2*)score, (const float2*)noise, seed, offset, coef, HW, total,
+                     (float2*)x_out, (float2*)xmean_out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int snrse_temb_mlp(const float* t, const float* Wg, const float* W1, const float* b1,
+                              const float* W2, const float* b2, float* temb, int B, int nf, hipStream_t s) {
+  if (nf != 128 || B <= 0) return SNRSE_EINVAL;
+  hipLaunchKernelGGL(temb_mlp_kernel, dim3(B), dim3(512), 0, s, t, Wg, W1, b1, W2, b2, temb, nf);
+  return (int)hipGetLastError();
+}
+
+extern "C" int snrse_temb_dense(const float* temb, const float* W, const float* bias, float* out, int B, int R,
+                                int D, hipStream_t s) {
+  if (D > 512 || B <= 0 || (size_t)B * D * 4 > 64 * 1024) return SNRSE_EINVAL;
+  hipLaunchKernelGGL(temb_dense_kernel, dim3((R + 63) / 64), dim3(256), sizeof(float) * B * D, s, temb, W, bias,
+                     out, B, R, D);
+  return (int)hipGetLastError();
+}
+
+extern "C" int snrse_input_pack(const void* x, const void* y, int B, int H, int W, void* col, float* pyr,
+                                int dtype, hipStream_t s) {
+  const int total = B * H * W;
+  if (total <= 0) return SNRSE_EINVAL;
+  dim3 grid((total + 255) / 256);
+  if (dtype == SNRSE_BF16)
+    hipLaunchKernelGGL(input_pack_kernel<bf16_t>, grid, dim3(256), 0, s, (const float2*)x, (const float2*)y, H, W,
+                       (bf16_t*)col, pyr, total);
+  else if (dtype == SNRSE_F32)
+    hipLaunchKernelGGL(input_pack_kernel<float>, grid, dim3(256), 0, s, (const float2*)x, (const float2*)y, H, W,
+                       (float*)col, pyr, total);
+  else
+    return SNRSE_EINVAL;
+  return (int)hipGetLastError();
+}
+
+extern "C" int snrse_score_update(const void* pyr, int pyr_f32, const float* out_w, const float* out_b,
+                                  const float* t, int score_mode, int B, int HW, const void* x, const void* y,
+                                  const void* noise, uint64_t seed, uint64_t offset, const float* coef,
+                                  void* x_out, void* xmean_out, void* score_out, hipStream_t s) {
+  const int total = B * HW;
+  if (total <= 0 || !pyr || !x) return SNRSE_EINVAL;
+  if (x_out && !coef) return SNRSE_EINVAL;
+  dim3 grid((total + 255) / 256);
+  if (pyr_f32)
+    hipLaunchKernelGGL(score_update_kernel<float>, grid, dim3(256), 0, s, (const float*)pyr, out_w, out_b, t,
+                       score_mode, HW, total, (const float2*)x, (const float2*)y, (const float2*)noise, seed,
+                       offset, coef, (float2*)x_out, (float2*)xmean_out, (float2*)score_out);
+  else
+    hipLaunchKernelGGL(score_update_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)pyr, out_w, out_b, t,
+                       score_mode, HW, total, (const float2*)x, (const float2*)y, (const float2*)noise, seed,
+                       offset, coef, (float2*)x_out, (float2*)xmean_out, (float2*)score_out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int snrse_axpby_noise(const void* x, const void* y, const void* noise, uint64_t seed, uint64_t offset,
+                                 const float* coef, int B, int HW, void* out, hipStream_t s) {
+  const int total = B * HW;
+  if (total <= 0 || !coef || !out) return SNRSE_EINVAL;
+  hipLaunchKernelGGL(axpby_noise_kernel, dim3((total + 255) / 256), dim3(256), 0, s, (const float2*)x,
+                     (const float2*)y, (const float2*)noise, seed, offset, coef, HW, total, (float2*)out);
+  return (int)hipGetLastError();
+}

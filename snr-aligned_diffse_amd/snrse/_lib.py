@@ -1,0 +1,80 @@
+"""ctypes binding of libsnrse_hip.so (include/snrse.h) — the only route to the kernels.
+
+There is deliberately no CPU fallback: if the library or a HIP device is missing, every
+op raises.  Tensors cross the boundary as raw device pointers (`data_ptr()`); launches go
+on torch's current HIP stream so torch events / graphs see them.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+# torch bundles its own libamdhip64.so.7; importing it first makes our library bind to that
+# same HIP runtime (same SONAME) instead of pulling /opt/rocm's copy into the process as a
+# second runtime whose device pointers and streams torch could not use.
+import torch  # noqa: F401
+
+from .build import LIB
+
+F32, BF16 = 0, 1
+
+_vp, _i, _f, _u64 = C.c_void_p, C.c_int, C.c_float, C.c_uint64
+
+# name -> argtypes (all return int status except the housekeeping ones)
+SIGNATURES = {
+    "snrse_upfirdn2d": [_vp, _vp, _vp] + [_i] * 15 + [_vp],
+    "snrse_conv2d": [_vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _i, _vp, _i, _f,
+                     _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp],
+    "snrse_gn_stats": [_vp, _i, _vp, _i, _i, _i, _vp, _i, _vp],
+    "snrse_gn_apply": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _f, _i, _i, _vp, _i, _vp],
+    "snrse_attention": [_vp, _vp, _i, _i, _i, _i, _vp],
+    "snrse_temb_mlp": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp],
+    "snrse_temb_dense": [_vp, _vp, _vp, _vp, _i, _i, _i, _vp],
+    "snrse_input_pack": [_vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp],
+    "snrse_score_update": [_vp, _i, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp],
+    "snrse_sde_update": [_vp, _vp, _vp, _vp, _u64, _u64, _vp, _i, _i, _vp, _vp, _vp],
+    "snrse_axpby_noise": [_vp, _vp, _vp, _u64, _u64, _vp, _i, _i, _vp, _vp],
+    "snrse_stft": [_vp, _i, _i, _f, _i, _i, _vp, _vp],
+    "snrse_istft": [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
+}
+HOUSEKEEPING = {"snrse_abi_version": ([], _i), "snrse_error_string": ([_i], C.c_char_p),
+                "snrse_device_name": ([C.c_char_p, _i], _i)}
+
+_lib = None
+
+
+def load(path: str | None = None) -> C.CDLL:
+    """Load (once) and type the library.  Raises OSError when it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or os.environ.get("SNRSE_LIB", LIB)
+    if not os.path.exists(path):
+        raise OSError(f"libsnrse_hip.so not found at {path}: run __graft_entry__.build() "
+                      "(or python -m snrse.build) first; there is no CPU fallback")
+    lib = C.CDLL(path)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _i
+    for name, (args, res) in HOUSEKEEPING.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(SIGNATURES) + list(HOUSEKEEPING)
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().snrse_error_string(rc)
+        raise RuntimeError(f"{what} failed: {msg.decode() if msg else rc} (code {rc})")
+
+
+def call(name: str, *args):
+    lib = load()
+    check(getattr(lib, name)(*args), name)

@@ -1,0 +1,256 @@
+"""NCSN++ score network executed on the HIP kernels (NHWC, bf16 or exact-fp32 mode).
+
+Mirrors NCSNpp (reference sgmse/backbones/ncsnpp.py:36-404) for its shipped configuration:
+nf=128, ch_mult=(1,1,2,2,2,2,2), num_res_blocks=2, attn_resolutions=(16,), BigGAN
+ResBlocks with FIR [1,3,3,1] resampling, skip_rescale, output_skip / input_skip pyramids
+with 'sum' combine, Gaussian-Fourier time embedding, 4-channel complex I/O.
+
+Each ResnetBlockBigGANpp (layerspp.py:244-276) runs as
+    stats(x) -> GN0+SiLU(+FIR) -> Conv_0 (+bias +Dense_0 temb)      [one MFMA GEMM]
+    stats(h) -> GN1+SiLU       -> Conv_1 (+bias) [+Conv_2 1x1 shortcut as extra K]
+                               -> (x + h)/sqrt(2) [+ input-skip Combine]    [one MFMA GEMM]
+and AttnBlockpp (layerspp.py:77-93) as GN -> fused QKV GEMM -> flash attention -> NIN_3
+GEMM with the residual epilogue.  Weights are re-packed once on the device (K-contiguous
+[Cout][ky][kx][Cin]).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from . import ops
+
+INV_SQRT2 = 1.0 / math.sqrt(2.0)
+
+
+@dataclass
+class Mod:
+    kind: str  # gfp, linear, conv3x3, rb, attn, combine, gn
+    idx: int
+    cin: int = 0
+    cout: int = 0
+    up: bool = False
+    down: bool = False
+    extra: dict = field(default_factory=dict)
+
+
+def build_plan(nf=128, ch_mult=(1, 1, 2, 2, 2, 2, 2), num_res_blocks=2, attn_resolutions=(16,),
+               image_size=256):
+    """Module list of NCSNpp.__init__ (ncsnpp.py:99-245) for the supported configuration."""
+    mods = []
+
+    def add(kind, **kw):
+        mods.append(Mod(kind, len(mods), **kw))
+
+    nres = len(ch_mult)
+    res = [image_size // (2 ** i) for i in range(nres)]
+    add("gfp", cout=2 * nf)
+    add("linear", cin=2 * nf, cout=4 * nf)
+    add("linear", cin=4 * nf, cout=4 * nf)
+    add("conv3x3", cin=4, cout=nf)
+    hs_c = [nf]
+    in_ch = nf
+    for lvl in range(nres):
+        for _ in range(num_res_blocks):
+            out_ch = nf * ch_mult[lvl]
+            add("rb", cin=in_ch, cout=out_ch)
+            in_ch = out_ch
+            if res[lvl] in attn_resolutions:
+                add("attn", cin=in_ch, cout=in_ch)
+            hs_c.append(in_ch)
+        if lvl != nres - 1:
+            add("rb", cin=in_ch, cout=in_ch, down=True)
+            add("combine", cin=4, cout=in_ch)
+            hs_c.append(in_ch)
+    in_ch = hs_c[-1]
+    add("rb", cin=in_ch, cout=in_ch)
+    add("attn", cin=in_ch, cout=in_ch)
+    add("rb", cin=in_ch, cout=in_ch)
+    for lvl in reversed(range(nres)):
+        for _ in range(num_res_blocks + 1):
+            out_ch = nf * ch_mult[lvl]
+            skip = hs_c.pop()
+            add("rb", cin=in_ch + skip, cout=out_ch, extra={"c0": in_ch, "c1": skip})
+            in_ch = out_ch
+        if res[lvl] in attn_resolutions:
+            add("attn", cin=in_ch, cout=in_ch)
+        add("gn", cin=in_ch, cout=in_ch)
+        add("conv3x3", cin=in_ch, cout=4)
+        if lvl != 0:
+            add("rb", cin=in_ch, cout=in_ch, up=True)
+    assert not hs_c
+    return mods
+
+
+def _pack3x3(w, dt, npad=None):
+    co = w.shape[0]
+    p = w.permute(0, 2, 3, 1).reshape(co, -1)
+    if npad is not None and npad > co:
+        p = torch.cat([p, p.new_zeros(npad - co, p.shape[1])], 0)
+    return p.to(dt).contiguous()
+
+
+def _pack1x1(w, dt, npad=None):
+    return _pack3x3(w, dt, npad)
+
+
+class NCSNppHIP:
+    """Device-resident packed weights + the forward executor."""
+
+    def __init__(self, sd: dict, dtype=torch.bfloat16, device="cuda", **cfg):
+        if not torch.cuda.is_available():
+            raise RuntimeError("snrse: NCSNppHIP needs a HIP device (no CPU fallback)")
+        self.dtype = dtype
+        self.device = torch.device(device)
+        self.plan = build_plan(**cfg)
+        dev, dt = self.device, dtype
+        f32 = lambda k: sd[k].detach().to(dev, torch.float32).contiguous()  # noqa: E731
+        self.W = {}
+        W = self.W
+        W["gfp"] = f32("all_modules.0.W")
+        W["l1w"], W["l1b"] = f32("all_modules.1.weight"), f32("all_modules.1.bias")
+        W["l2w"], W["l2b"] = f32("all_modules.2.weight"), f32("all_modules.2.bias")
+        w_in = sd["all_modules.3.weight"].detach().to(dev, torch.float32)  # [128, 4, 3, 3]
+        col = w_in.permute(0, 2, 3, 1).reshape(w_in.shape[0], 36)
+        W["in_w"] = torch.cat([col, col.new_zeros(col.shape[0], 28)], 1).to(dt).contiguous()
+        W["in_b"] = f32("all_modules.3.bias")
+        W["out_w"] = f32("output_layer.weight").reshape(2, 4).contiguous()
+        W["out_b"] = f32("output_layer.bias")
+        dense_w, dense_b, off = [], [], 0
+        self.mw = {}
+        for m in self.plan:
+            pre = f"all_modules.{m.idx}"
+            e = {}
+            if m.kind == "rb":
+                e["gn0_g"], e["gn0_b"] = f32(pre + ".GroupNorm_0.weight"), f32(pre + ".GroupNorm_0.bias")
+                e["gn1_g"], e["gn1_b"] = f32(pre + ".GroupNorm_1.weight"), f32(pre + ".GroupNorm_1.bias")
+                e["w0"] = _pack3x3(sd[pre + ".Conv_0.weight"].detach().to(dev), dt)
+                e["b0"] = f32(pre + ".Conv_0.bias")
+                e["w1"] = _pack3x3(sd[pre + ".Conv_1.weight"].detach().to(dev), dt)
+                b1 = f32(pre + ".Conv_1.bias")
+                if m.cin != m.cout or m.up or m.down:
+                    e["w2"] = _pack1x1(sd[pre + ".Conv_2.weight"].detach().to(dev), dt)
+                    b1 = b1 + f32(pre + ".Conv_2.bias")
+                e["b1"] = b1.contiguous()
+                dense_w.append(f32(pre + ".Dense_0.weight"))
+                dense_b.append(f32(pre + ".Dense_0.bias"))
+                e["temb_off"] = off
+                off += m.cout
+            elif m.kind == "attn":
+                e["gn_g"], e["gn_b"] = f32(pre + ".GroupNorm_0.weight"), f32(pre + ".GroupNorm_0.bias")
+                Ws = [sd[f"{pre}.NIN_{i}.W"].detach().to(dev, torch.float32) for i in range(4)]
+                e["wqkv"] = torch.cat([Ws[0].t(), Ws[1].t(), Ws[2].t()], 0).to(dt).contiguous()
+                e["bqkv"] = torch.cat([f32(f"{pre}.NIN_{i}.b") for i in range(3)]).contiguous()
+                e["w3"] = Ws[3].t().to(dt).contiguous()
+                e["b3"] = f32(pre + ".NIN_3.b")
+            elif m.kind == "combine":
+                e["w"] = f32(pre + ".Conv_0.weight").reshape(m.cout, 4).contiguous()
+                e["b"] = f32(pre + ".Conv_0.bias")
+            elif m.kind == "gn":
+                e["g"], e["b"] = f32(pre + ".weight"), f32(pre + ".bias")
+            elif m.kind == "conv3x3" and m.idx != 3:
+                e["w"] = _pack3x3(sd[pre + ".weight"].detach().to(dev), dt, npad=16)
+                e["b"] = f32(pre + ".bias")
+            self.mw[m.idx] = e
+        W["dense_w"] = torch.cat(dense_w, 0).contiguous()
+        W["dense_b"] = torch.cat(dense_b, 0).contiguous()
+
+    # ------------------------------------------------------------------ blocks
+    def _resblock(self, m, x0, x1, dense, comb=None, comb_w=None, comb_b=None):
+        e = self.mw[m.idx]
+        mode = "up" if m.up else ("down" if m.down else "none")
+        s0 = ops.gn_stats(x0, x1)
+        a0 = ops.gn_apply(x0, x1, s0, e["gn0_g"], e["gn0_b"], act=True, mode=mode)
+        h = ops.conv2d(a0, e["w0"], 3, m.cout, bias=e["b0"], temb=dense, temb_off=e["temb_off"])
+        s1 = ops.gn_stats(h)
+        a1 = ops.gn_apply(h, None, s1, e["gn1_g"], e["gn1_b"], act=True)
+        if "w2" in e:
+            if mode != "none":
+                xs0, xs1 = ops.fir(x0 if x1 is None else torch.cat([x0, x1], 3), mode), None
+            else:
+                xs0, xs1 = x0, x1
+            return ops.conv2d(a1, e["w1"], 3, m.cout, bias=e["b1"], sc=xs0, sc1=xs1, sc_wgt=e["w2"],
+                              out_scale=INV_SQRT2, comb=comb, comb_w=comb_w, comb_b=comb_b)
+        assert x1 is None
+        return ops.conv2d(a1, e["w1"], 3, m.cout, bias=e["b1"], res=x0, out_scale=INV_SQRT2,
+                          comb=comb, comb_w=comb_w, comb_b=comb_b)
+
+    def _attn(self, m, x):
+        e = self.mw[m.idx]
+        s = ops.gn_stats(x)
+        a = ops.gn_apply(x, None, s, e["gn_g"], e["gn_b"], act=False)
+        qkv = ops.conv2d(a, e["wqkv"], 1, 3 * m.cout, bias=e["bqkv"])
+        o = ops.attention(qkv, m.cout)
+        return ops.conv2d(o, e["w3"], 1, m.cout, bias=e["b3"], res=x, out_scale=INV_SQRT2)
+
+    def _pyramid_head(self, gn_m, conv_m, h, pyr_up):
+        g = self.mw[gn_m.idx]
+        c = self.mw[conv_m.idx]
+        s = ops.gn_stats(h)
+        a = ops.gn_apply(h, None, s, g["g"], g["b"], act=True)
+        return ops.conv2d(a, c["w"], 3, 4, bias=c["b"], res=pyr_up, out_f32=True)
+
+    # ------------------------------------------------------------------ forward
+    def temb(self, t):
+        W = self.W
+        temb = ops.temb_mlp(t, W["gfp"], W["l1w"], W["l1b"], W["l2w"], W["l2b"])
+        return ops.temb_dense(temb, W["dense_w"], W["dense_b"])
+
+    def pyramid(self, x, y, t):
+        """x, y complex64 [B,F,T] (contiguous, device); t [B] f32 -> final pyramid [B,F,T,4] f32
+        (ncsnpp.py:389-398 before the division by t and the output layer)."""
+        W = self.W
+        dense = self.temb(t)
+        col, pyr_in = ops.input_pack(x, y, self.dtype)
+        h = ops.conv2d(col, W["in_w"], 1, 128, bias=W["in_b"])
+        hs = [h]
+        plan = self.plan
+        i = 4
+        nres = 7
+        for lvl in range(nres):
+            for _ in range(2):
+                h = self._resblock(plan[i], hs[-1], None, dense)
+                i += 1
+                if plan[i].kind == "attn":
+                    h = self._attn(plan[i], h)
+                    i += 1
+                hs.append(h)
+            if lvl != nres - 1:
+                rb, cmb = plan[i], plan[i + 1]
+                pyr_in = ops.fir(pyr_in, "down")
+                ce = self.mw[cmb.idx]
+                h = self._resblock(rb, hs[-1], None, dense, comb=pyr_in, comb_w=ce["w"], comb_b=ce["b"])
+                i += 2
+                hs.append(h)
+        h = hs[-1]
+        h = self._resblock(plan[i], h, None, dense); i += 1  # noqa: E702
+        h = self._attn(plan[i], h); i += 1  # noqa: E702
+        h = self._resblock(plan[i], h, None, dense); i += 1  # noqa: E702
+        pyr = None
+        for lvl in reversed(range(nres)):
+            for _ in range(3):
+                h = self._resblock(plan[i], h, hs.pop(), dense)
+                i += 1
+            if plan[i].kind == "attn":
+                h = self._attn(plan[i], h)
+                i += 1
+            pyr_up = None if pyr is None else ops.fir(pyr, "up")
+            pyr = self._pyramid_head(plan[i], plan[i + 1], h, pyr_up)
+            i += 2
+            if lvl != 0:
+                h = self._resblock(plan[i], h, None, dense)
+                i += 1
+        assert i == len(plan) and not hs
+        return pyr
+
+    def score(self, x, y, t, score_mode=0):
+        """Preconditioned score (ScoreModel.forward, model.py:481-543) as complex64 [B,F,T]."""
+        pyr = self.pyramid(x, y, t)
+        _, _, sc = ops.score_update(pyr, self.W["out_w"], self.W["out_b"], t, score_mode, x, y, want_score=True)
+        return sc
+
+    def dnn(self, x, y, t):
+        """Raw NCSNpp.forward output (no sign / preconditioning): complex64 [B,F,T]."""
+        return -self.score(x, y, t, score_mode=0)

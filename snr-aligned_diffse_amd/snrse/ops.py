@@ -1,0 +1,207 @@
+"""Torch-tensor wrappers over the C-ABI (device pointers + torch's current stream).
+
+Every op requires HIP device tensors and raises otherwise — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+
+F32, BF16 = _lib.F32, _lib.BF16
+INV_SQRT2 = 1.0 / math.sqrt(2.0)
+
+
+def code(dtype: torch.dtype) -> int:
+    if dtype == torch.float32:
+        return F32
+    if dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"snrse: unsupported dtype {dtype}")
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("snrse: HIP device tensor required (no CPU fallback)")
+        if t is not None and not t.is_contiguous():
+            raise RuntimeError("snrse: contiguous tensor required")
+
+
+def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_wgt=None, temb=None,
+           temb_off=0, res=None, out_scale=1.0, comb=None, comb_w=None, comb_b=None, out=None,
+           out_f32=False):
+    """NHWC conv (see snrse_conv2d).  src0 [B,H,W,C0]; returns out [B,H,W,cout].
+    temb: [B, R] f32 table of all Dense_0 outputs, this layer's columns start at temb_off."""
+    _dev(src0, src1, wgt, sc, sc1, sc_wgt, bias, res, comb, comb_w, comb_b, temb)
+    B, H, W, C0 = src0.shape
+    C1 = 0 if src1 is None else src1.shape[3]
+    Csc = 0 if sc is None else sc.shape[3]
+    Csc1 = 0 if sc1 is None else sc1.shape[3]
+    odt = torch.float32 if out_f32 else src0.dtype
+    if out is None:
+        out = torch.empty(B, H, W, cout, device=src0.device, dtype=odt)
+    _lib.call("snrse_conv2d", _ptr(src0), C0, _ptr(src1), C1, B, H, W, ksize, _ptr(wgt), _ptr(sc), Csc,
+              _ptr(sc1), Csc1, _ptr(sc_wgt), _ptr(bias), None if temb is None else temb.data_ptr() + 4 * temb_off,
+              0 if temb is None else temb.shape[1], _ptr(res), 0 if res is None else res.shape[-1], float(out_scale), _ptr(comb),
+              _ptr(comb_w), _ptr(comb_b), out.data_ptr(), cout, out.shape[-1], code(src0.dtype),
+              int(out_f32), _stream())
+    return out
+
+
+def gn_stats(src0, src1=None):
+    _dev(src0, src1)
+    B, H, W, C0 = src0.shape
+    C1 = 0 if src1 is None else src1.shape[3]
+    sums = torch.empty(B, C0 + C1, 2, device=src0.device, dtype=torch.float64)
+    _lib.call("snrse_gn_stats", _ptr(src0), C0, _ptr(src1), C1, B, H * W, sums.data_ptr(),
+              code(src0.dtype), _stream())
+    return sums
+
+
+MODES = {"none": 0, "down": 1, "up": 2}
+
+
+def gn_apply(src0, src1=None, sums=None, gamma=None, beta=None, act=True, mode="none", groups=None, eps=1e-6):
+    _dev(src0, src1, sums, gamma, beta)
+    B, H, W, C0 = src0.shape
+    C1 = 0 if src1 is None else src1.shape[3]
+    C = C0 + C1
+    m = MODES[mode]
+    Ho, Wo = (H // 2, W // 2) if m == 1 else ((2 * H, 2 * W) if m == 2 else (H, W))
+    out = torch.empty(B, Ho, Wo, C, device=src0.device, dtype=src0.dtype)
+    g = groups if groups is not None else min(C // 4, 32)
+    _lib.call("snrse_gn_apply", _ptr(src0), C0, _ptr(src1), C1, B, H, W, _ptr(sums), _ptr(gamma), _ptr(beta),
+              g, float(eps), int(bool(act)), m, out.data_ptr(), code(src0.dtype), _stream())
+    return out
+
+
+def fir(x, mode):
+    """FIR [1,3,3,1] down/up x2 of an NHWC tensor (no normalisation)."""
+    return gn_apply(x, act=False, mode=mode)
+
+
+def attention(qkv, C=256):
+    _dev(qkv)
+    B, L = qkv.shape[0], qkv.shape[1] * (qkv.shape[2] if qkv.dim() == 4 else 1)
+    out = torch.empty(*qkv.shape[:-1], C, device=qkv.device, dtype=qkv.dtype)
+    _lib.call("snrse_attention", qkv.data_ptr(), out.data_ptr(), B, L, C, code(qkv.dtype), _stream())
+    return out
+
+
+def temb_mlp(t, Wg, W1, b1, W2, b2):
+    _dev(t, Wg, W1, b1, W2, b2)
+    B = t.shape[0]
+    out = torch.empty(B, W2.shape[0], device=t.device, dtype=torch.float32)
+    _lib.call("snrse_temb_mlp", t.data_ptr(), Wg.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
+              b2.data_ptr(), out.data_ptr(), B, Wg.shape[0], _stream())
+    return out
+
+
+def temb_dense(temb, W, bias):
+    _dev(temb, W, bias)
+    B, D = temb.shape
+    R = W.shape[0]
+    out = torch.empty(B, R, device=temb.device, dtype=torch.float32)
+    _lib.call("snrse_temb_dense", temb.data_ptr(), W.data_ptr(), bias.data_ptr(), out.data_ptr(), B, R, D,
+              _stream())
+    return out
+
+
+def input_pack(x, y, dtype):
+    """x, y complex64 [B,F,T] -> (im2col [B,F,T,64] dtype, pyramid [B,F,T,4] f32)."""
+    _dev(x, y)
+    B, F, T = x.shape[0], x.shape[-2], x.shape[-1]
+    col = torch.empty(B, F, T, 64, device=x.device, dtype=dtype)
+    pyr = torch.empty(B, F, T, 4, device=x.device, dtype=torch.float32)
+    _lib.call("snrse_input_pack", x.data_ptr(), y.data_ptr(), B, F, T, col.data_ptr(), pyr.data_ptr(),
+              code(dtype), _stream())
+    return col, pyr
+
+
+def score_update(pyr, out_w, out_b, t, score_mode, x, y=None, coef=None, noise=None, seed=0, offset=0,
+                 want_score=False, x_out=None, xmean_out=None):
+    """Output head + score + optional SDE step.  Returns (x_out, x_mean, score)."""
+    _dev(pyr, out_w, out_b, t, x, y, coef, noise)
+    B = x.shape[0]
+    HW = x.shape[-2] * x.shape[-1]
+    score = torch.empty_like(x) if want_score else None
+    if coef is not None:
+        x_out = torch.empty_like(x) if x_out is None else x_out
+        xmean_out = torch.empty_like(x) if xmean_out is None else xmean_out
+    else:
+        x_out = xmean_out = None
+    _lib.call("snrse_score_update", pyr.data_ptr(), int(pyr.dtype == torch.float32), out_w.data_ptr(),
+              out_b.data_ptr(), t.data_ptr(), int(score_mode), B, HW, x.data_ptr(), _ptr(y), _ptr(noise),
+              int(seed) & (2**64 - 1), int(offset), _ptr(coef), _ptr(x_out), _ptr(xmean_out), _ptr(score),
+              _stream())
+    return x_out, xmean_out, score
+
+
+def sde_update(x, coef, y=None, score=None, noise=None, seed=0, offset=0, x_out=None, xmean_out=None):
+    _dev(x, coef, y, score, noise)
+    B = x.shape[0]
+    HW = x.shape[-2] * x.shape[-1]
+    x_out = torch.empty_like(x) if x_out is None else x_out
+    xmean_out = torch.empty_like(x) if xmean_out is None else xmean_out
+    _lib.call("snrse_sde_update", x.data_ptr(), _ptr(y), _ptr(score), _ptr(noise), int(seed) & (2**64 - 1),
+              int(offset), coef.data_ptr(), B, HW, x_out.data_ptr(), xmean_out.data_ptr(), _stream())
+    return x_out, xmean_out
+
+
+def axpby_noise(coef, x=None, y=None, noise=None, seed=0, offset=0, like=None):
+    ref = x if x is not None else (y if y is not None else like)
+    _dev(coef, x, y, noise)
+    B = ref.shape[0]
+    HW = ref.shape[-2] * ref.shape[-1]
+    out = torch.empty_like(ref)
+    _lib.call("snrse_axpby_noise", _ptr(x), _ptr(y), _ptr(noise), int(seed) & (2**64 - 1), int(offset),
+              coef.data_ptr(), B, HW, out.data_ptr(), _stream())
+    return out
+
+
+def stft(sig, in_scale=1.0, tpad=None, mode=1):
+    """sig [B, L] f32 -> complex64 [B, 256, Tpad]."""
+    _dev(sig)
+    B, L = sig.shape
+    T = 1 + L // 128
+    tpad = T if tpad is None else tpad
+    out = torch.empty(B, 256, tpad, device=sig.device, dtype=torch.complex64)
+    _lib.call("snrse_stft", sig.data_ptr(), B, L, float(in_scale), tpad, int(mode), out.data_ptr(), _stream())
+    return out
+
+
+def istft(spec, length, mode=1, out_scale=None):
+    """spec complex64 [B, 256, T] -> [B, length] f32 (* out_scale[b])."""
+    _dev(spec, out_scale)
+    B, Fq, T = spec.shape
+    frames = torch.empty(B, T, 510, device=spec.device, dtype=torch.float32)
+    out = torch.empty(B, length, device=spec.device, dtype=torch.float32)
+    _lib.call("snrse_istft", spec.data_ptr(), B, T, length, int(mode), _ptr(out_scale), frames.data_ptr(),
+              out.data_ptr(), _stream())
+    return out
+
+
+def upfirdn2d(inp, kernel, up=1, down=1, pad=(0, 0)):
+    """Reference-signature upfirdn2d (op/upfirdn2d.py:145-156) on [N, C, H, W]."""
+    _dev(inp, kernel)
+    N, Cc, H, W = inp.shape
+    kh, kw = kernel.shape
+    x = inp.reshape(N * Cc, H, W, 1).contiguous()
+    oh = (H * up + pad[0] + pad[1] - kh) // down + 1
+    ow = (W * up + pad[0] + pad[1] - kw) // down + 1
+    out = torch.empty(N * Cc, oh, ow, 1, device=inp.device, dtype=inp.dtype)
+    k = kernel.to(torch.float32).contiguous()
+    _lib.call("snrse_upfirdn2d", x.data_ptr(), out.data_ptr(), k.data_ptr(), N * Cc, H, W, 1, kh, kw, up, up,
+              down, down, pad[0], pad[1], pad[0], pad[1], code(inp.dtype), _stream())
+    return out.view(N, Cc, oh, ow)

@@ -1,0 +1,293 @@
+"""Parity of the HIP kernels (through the C-ABI) against the CPU oracle / golden vectors.
+
+Tolerances: fp32 mode (exact f32 MFMA) is held to the north-star 1e-4 relative RMS on the
+complex spectrogram (and <= 1e-5 on single kernels); bf16 mode to 2e-2 relative RMS.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import fnormal, formula_attn_sd, formula_sd, golden
+from oracle import ncsnpp_ref, sde_ref, spec_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).detach().cpu().to(torch.complex128 if torch.is_complex(torch.as_tensor(a)) else torch.float64)
+    b = torch.as_tensor(b).detach().cpu().to(a.dtype)
+    return float((a - b).abs().pow(2).mean().sqrt() / (b.abs().pow(2).mean().sqrt() + 1e-30))
+
+
+def nhwc(x):  # [B,C,H,W] -> [B,H,W,C]
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(x):
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+DT = {"f32": (torch.float32, 2e-6), "bf16": (torch.bfloat16, 1e-2)}
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("shape", [(2, 128, 128, 8, 16), (1, 256, 128, 4, 8), (3, 128, 256, 5, 7), (2, 384, 256, 4, 4)])
+def test_conv3x3(gpu, dt, shape):
+    from snrse import ops
+    dtype, tol = DT[dt]
+    B, cin, cout, H, W = shape
+    x = torch.from_numpy(fnormal("t.conv.x", (B, cin, H, W)))
+    w = torch.from_numpy(fnormal("t.conv.w", (cout, cin, 3, 3))) / math.sqrt(9 * cin)
+    b = torch.from_numpy(fnormal("t.conv.b", (cout,)))
+    if dt == "bf16":
+        x, w = x.bfloat16().float(), w.bfloat16().float()
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1)
+    c0 = 256 if cin == 384 else cin
+    xg = nhwc(x).to(gpu, dtype)
+    src0, src1 = (xg[..., :c0].contiguous(), xg[..., c0:].contiguous()) if c0 != cin else (xg, None)
+    wp = w.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu, dtype).contiguous()
+    out = ops.conv2d(src0, wp, 3, cout, bias=b.to(gpu), src1=src1)
+    assert rel(nchw(out.float()), ref) < tol
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_conv_epilogue_shortcut_temb_comb(gpu, dt):
+    """Conv_1 + Conv_2 shortcut as extra K, temb bias, residual scale and Combine term."""
+    from snrse import ops
+    dtype, tol = DT[dt]
+    B, cin, cout, H, W = 2, 128, 256, 8, 8
+    h = torch.from_numpy(fnormal("t.ep.h", (B, cout, H, W)))
+    xs = torch.from_numpy(fnormal("t.ep.xs", (B, cin, H, W)))
+    w1 = torch.from_numpy(fnormal("t.ep.w1", (cout, cout, 3, 3))) / 48
+    w2 = torch.from_numpy(fnormal("t.ep.w2", (cout, cin, 1, 1))) / 11
+    b1 = torch.from_numpy(fnormal("t.ep.b1", (cout,)))
+    temb = torch.from_numpy(fnormal("t.ep.temb", (B, 300)))
+    pyr = torch.from_numpy(fnormal("t.ep.pyr", (B, 4, H, W)))
+    cw = torch.from_numpy(fnormal("t.ep.cw", (cout, 4)))
+    cb = torch.from_numpy(fnormal("t.ep.cb", (cout,)))
+    if dt == "bf16":
+        h, xs, w1, w2 = (v.bfloat16().float() for v in (h, xs, w1, w2))
+    ref = (F.conv2d(h.double(), w1.double(), b1.double(), padding=1) + F.conv2d(xs.double(), w2.double())
+           + temb[:, 20:20 + cout, None, None].double()) / math.sqrt(2)
+    ref = ref + torch.einsum("bihw,oi->bohw", pyr.double(), cw.double()) + cb.double()[None, :, None, None]
+    out = ops.conv2d(nhwc(h).to(gpu, dtype), w1.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu, dtype).contiguous(),
+                     3, cout, bias=b1.to(gpu), sc=nhwc(xs).to(gpu, dtype),
+                     sc_wgt=w2.reshape(cout, cin).to(gpu, dtype).contiguous(), temb=temb.to(gpu), temb_off=20,
+                     out_scale=1 / math.sqrt(2), comb=nhwc(pyr).to(gpu), comb_w=cw.to(gpu), comb_b=cb.to(gpu))
+    assert rel(nchw(out.float()), ref) < tol
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_conv_small_cout_pyramid(gpu, dt):
+    from snrse import ops
+    dtype, tol = DT[dt]
+    B, cin, H, W = 2, 256, 8, 16
+    x = torch.from_numpy(fnormal("t.py.x", (B, cin, H, W)))
+    w = torch.from_numpy(fnormal("t.py.w", (4, cin, 3, 3))) / 48
+    b = torch.from_numpy(fnormal("t.py.b", (4,)))
+    r = torch.from_numpy(fnormal("t.py.r", (B, 4, H, W)))
+    if dt == "bf16":
+        x, w = x.bfloat16().float(), w.bfloat16().float()
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1) + r.double()
+    wp = torch.cat([w.permute(0, 2, 3, 1).reshape(4, -1), torch.zeros(12, 9 * cin)]).to(gpu, dtype).contiguous()
+    out = ops.conv2d(nhwc(x).to(gpu, dtype), wp, 3, 4, bias=b.to(gpu), res=nhwc(r).to(gpu), out_f32=True)
+    assert out.dtype == torch.float32
+    assert rel(nchw(out), ref) < tol
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("mode", ["none", "down", "up"])
+@pytest.mark.parametrize("C", [128, 384])
+def test_gn_silu_fir(gpu, dt, mode, C):
+    from snrse import ops
+    dtype, tol = DT[dt]
+    B, H, W = 2, 8, 16
+    x = torch.from_numpy(fnormal("t.gn.x", (B, C, H, W))) * 2 + 0.3
+    g = torch.from_numpy(fnormal("t.gn.g", (C,))) * 0.1 + 1
+    be = torch.from_numpy(fnormal("t.gn.b", (C,))) * 0.1
+    if dt == "bf16":
+        x = x.bfloat16().float()
+    ref = F.silu(F.group_norm(x.double(), min(C // 4, 32), g.double(), be.double(), eps=1e-6))
+    if mode == "down":
+        ref = ncsnpp_ref.fir_down2(ref)
+    elif mode == "up":
+        ref = ncsnpp_ref.fir_up2(ref)
+    xg = nhwc(x).to(gpu, dtype)
+    s0, s1 = (xg[..., :256].contiguous(), xg[..., 256:].contiguous()) if C == 384 else (xg, None)
+    sums = ops.gn_stats(s0, s1)
+    out = ops.gn_apply(s0, s1, sums, g.to(gpu), be.to(gpu), act=True, mode=mode)
+    assert rel(nchw(out.float()), ref) < tol
+
+
+def test_upfirdn2d_reference_api(gpu):
+    from snrse import ops
+    g = golden("fir.npz")
+    x = torch.from_numpy(fnormal("golden.fir.x", (2, 8, 16, 32))).to(gpu)
+    k = torch.tensor([1.0, 3.0, 3.0, 1.0])
+    k2 = torch.outer(k, k)
+    k2 = k2 / k2.sum()
+    up = ops.upfirdn2d(x, (k2 * 4).to(gpu), up=2, pad=(2, 1))
+    dn = ops.upfirdn2d(x, k2.to(gpu), down=2, pad=(1, 1))
+    np.testing.assert_allclose(up.cpu().numpy(), g["up"], atol=1e-5)
+    np.testing.assert_allclose(dn.cpu().numpy(), g["down"], atol=1e-5)
+    np.testing.assert_allclose(nchw(ops.fir(nhwc(x), "up")).cpu().numpy(), g["up"], atol=1e-5)
+    np.testing.assert_allclose(nchw(ops.fir(nhwc(x), "down")).cpu().numpy(), g["down"], atol=1e-5)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("L", [128, 37, 512])
+def test_attention_core(gpu, dt, L):
+    from snrse import ops
+    dtype, tol = DT[dt]
+    B, C = 2, 256
+    qkv = torch.from_numpy(fnormal("t.at.qkv", (B, L, 3 * C)))
+    if dt == "bf16":
+        qkv = qkv.bfloat16().float()
+    q, k, v = qkv.double().split(C, dim=2)
+    p = torch.softmax(q @ k.transpose(1, 2) / 16.0, dim=-1)
+    ref = p @ v
+    out = ops.attention(qkv.to(gpu, dtype).contiguous(), C)
+    assert rel(out.float(), ref) < (tol if dt == "f32" else 2e-2)
+
+
+def test_attn_block_golden(gpu):
+    from snrse import ops
+    g = golden("attn.npz")
+    sd = {k: torch.from_numpy(v) for k, v in formula_attn_sd("attn.").items()}
+    x = torch.from_numpy(fnormal("golden.attn.x", (2, 256, 16, 8)))
+    xg = nhwc(x).to(gpu)
+    s = ops.gn_stats(xg)
+    a = ops.gn_apply(xg, None, s, sd["GroupNorm_0.weight"].to(gpu), sd["GroupNorm_0.bias"].to(gpu), act=False)
+    wqkv = torch.cat([sd[f"NIN_{i}.W"].t() for i in range(3)], 0).to(gpu).contiguous()
+    bqkv = torch.cat([sd[f"NIN_{i}.b"] for i in range(3)]).to(gpu)
+    qkv = ops.conv2d(a, wqkv, 1, 768, bias=bqkv)
+    o = ops.attention(qkv, 256)
+    out = ops.conv2d(o, sd["NIN_3.W"].t().contiguous().to(gpu), 1, 256, bias=sd["NIN_3.b"].to(gpu), res=xg,
+                     out_scale=1 / math.sqrt(2))
+    assert rel(nchw(out), g["out"]) < 1e-5
+
+
+@pytest.fixture(scope="module")
+def sd_ncsnpp():
+    return {k: torch.from_numpy(v) for k, v in formula_sd("ncsnpp").items()}
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_ncsnpp_full_golden(gpu, sd_ncsnpp, dt):
+    from snrse import ncsnpp
+    g = golden("ncsnpp_full.npz")
+    net = ncsnpp.NCSNppHIP(sd_ncsnpp, dtype=DT[dt][0])
+    x = torch.from_numpy(fnormal("golden.ncsnpp.x", (2, 2, 256, 64), complex_=True)) * 0.5
+    t = torch.tensor([0.5, 0.8], device=gpu)
+    xg, yg = x[:, 0].contiguous().to(gpu), x[:, 1].contiguous().to(gpu)
+    out = net.dnn(xg, yg, t)
+    err = rel(out, g["out"][:, 0])
+    assert err < (1e-4 if dt == "f32" else 2e-2), err
+
+
+def test_stft_istft_golden(gpu):
+    from snrse import ops
+    g = golden("stft.npz")
+    y = torch.from_numpy(g["noisy_i16"].astype(np.float32) / 32768.0)[None]
+    nf = float(y.abs().max())
+    yg = y.to(gpu)
+    raw = ops.stft(yg, 1.0 / nf, mode=0)
+    assert rel(raw, g["stft"]) < 1e-5
+    spec = ops.stft(yg, 1.0 / nf, mode=1)
+    assert rel(spec, g["spec_fwd"]) < 2e-5
+    T = spec.shape[-1]
+    Tp = T + (64 - T % 64) % 64
+    spec_p = ops.stft(yg, 1.0 / nf, tpad=Tp, mode=1)
+    assert torch.all(spec_p[..., T:] == 0)
+    rt = ops.istft(spec, y.shape[1], mode=1)
+    np.testing.assert_allclose(rt.cpu().numpy()[0], g["roundtrip"][0], atol=2e-5)
+    Yp = spec_ref.pad_spec(g["spec_fwd"][:, None])[:, 0]
+    Yp = Yp + 0.01 * fnormal("golden.stft.pert", Yp.shape, complex_=True)
+    w = ops.istft(torch.from_numpy(Yp.astype(np.complex64)).to(gpu), y.shape[1], mode=1)
+    np.testing.assert_allclose(w.cpu().numpy()[0], g["istft_padded"], atol=3e-5)
+
+
+def test_stft_batch_edge_lengths(gpu):
+    """Ragged lengths (not multiples of the hop) through the batched STFT/iSTFT vs fp64 oracle."""
+    from snrse import ops
+    for L in (300, 1000, 16001, 27861):
+        sig = fnormal(f"t.stft.{L}", (3, L)) * 0.3
+        ref = spec_ref.stft(sig)
+        out = ops.stft(torch.from_numpy(sig).to(gpu), 1.0, mode=0)
+        assert rel(out, ref) < 1e-5
+        back = ops.istft(out, L, mode=0)
+        assert rel(back, spec_ref.istft(ref, L)) < 1e-5
+
+
+class Tape:
+    def __init__(self, tag, device):
+        self.tag, self.device = tag, device
+
+    def __call__(self, i, shape):
+        return torch.from_numpy(fnormal(f"{self.tag}.{i}", tuple(shape), complex_=True)).to(self.device)
+
+
+def test_pc_variants_generic(gpu):
+    """Every pinned predictor/corrector pairing through snrse_sde_update with an analytic score."""
+    from snrse import ops, sampler
+    g = golden("pc_variants.npz")
+    Y = torch.from_numpy(fnormal("golden.pcv.Y", (2, 1, 16, 8), complex_=True))[:, 0].contiguous().to(gpu)
+
+    def score_tensor(x, t):
+        return (-(x - Y[: x.shape[0]]) * 0.7 + 0.1 * Y[: x.shape[0]]).contiguous()
+
+    for key in [k for k in g.files if "__" in k and not k.endswith(("__ns", "__draws"))]:
+        sde_name, pred, corr = key.split("__")
+        sde = sampler.SDESpec("ouve") if sde_name == "ouve" else sampler.SDESpec("bbed")
+        Yc = Y if sde_name == "ouve" else Y[:1].contiguous()
+        tape = Tape(f"golden.pcv.{sde_name}.{pred}.{corr}", gpu)
+        shape = (Yc.shape[0], 1) + tuple(Yc.shape[1:])
+
+        def step(x, tv, coef, z, seed, off):
+            return ops.sde_update(x, coef, y=Yc, score=score_tensor(x, tv), noise=z)
+
+        src = sampler.NoiseSource(tape=lambda i: tape(i, shape).reshape(Yc.shape))
+        xr, ns = sampler.pc_sample(step, Yc, sde, N=6, predictor=pred, corrector=corr, noise=src,
+                                   score_tensor=score_tensor)
+        assert ns == int(g[key + "__ns"]) and src.i == int(g[key + "__draws"]), key
+        tol = 2e-6 if sde_name == "ouve" else 3e-5
+        assert rel(xr, g[key][:, 0]) < tol, (key, rel(xr, g[key][:, 0]))
+
+
+def test_pc_ouve_network_golden(gpu, sd_ncsnpp):
+    """Reference PC run (reverse_diffusion + ald, OUVE, N=5, B=2) on the full network, fp32."""
+    from snrse import ncsnpp, ops, sampler
+    g = golden("pc_ouve.npz")
+    net = ncsnpp.NCSNppHIP(sd_ncsnpp, dtype=torch.float32)
+    Y = (torch.from_numpy(fnormal("golden.pc.Y", (2, 1, 256, 64), complex_=True)) * 0.5)[:, 0].contiguous().to(gpu)
+
+    def step(x, tv, coef, z, seed, off):
+        pyr = net.pyramid(x, Y, tv)
+        xo, xm, _ = ops.score_update(pyr, net.W["out_w"], net.W["out_b"], tv, 0, x, Y, coef=coef, noise=z,
+                                     seed=seed, offset=off)
+        return xo, xm
+
+    tape = Tape("golden.pc.noise", gpu)
+    src = sampler.NoiseSource(tape=lambda i: tape(i, (2, 1, 256, 64)).reshape(Y.shape))
+    xr, ns = sampler.pc_sample(step, Y, sampler.SDESpec("ouve", theta=1.5, sigma_min=0.05, sigma_max=0.5), N=5,
+                               noise=src)
+    assert ns == 10 and src.i == 11
+    err = rel(xr, g["out"][:, 0])
+    assert err < 1e-4, err
+
+
+def test_philox_noise_statistics(gpu):
+    from snrse import ops
+    B, HW = 4, 256 * 512
+    coef = torch.tensor([[0.0, 0.0, 0.0, 1.0]] * B, device=gpu)
+    like = torch.empty(B, 256, 512, dtype=torch.complex64, device=gpu)
+    z = ops.axpby_noise(coef, like=like, seed=1234, offset=0)
+    z2 = ops.axpby_noise(coef, like=like, seed=1234, offset=0)
+    z3 = ops.axpby_noise(coef, like=like, seed=1234, offset=z.numel())
+    assert torch.equal(z, z2) and not torch.equal(z, z3)
+    r = torch.view_as_real(z).double()
+    assert abs(float(r.mean())) < 2e-3
+    assert abs(float(r.var()) - 0.5) < 2e-3
