@@ -106,11 +106,15 @@ int snrse_sde_update(const void* x, const void* y, const void* score, const void
 int snrse_axpby_noise(const void* x, const void* y, const void* noise, uint64_t seed, uint64_t offset,
                       const float* coef, int B, int HW, void* out, hipStream_t stream);
 
+/* norm_factor = max |y| per utterance (model.py:726): out[b] = max_i |sig[b][i]|. */
+int snrse_absmax(const float* sig, int B, int L, float* out, hipStream_t stream);
+
 /* STFT (data_module.py:291-293 with spec_fwd 241-254 and pad_spec other.py:83-90):
  * sig [B][L] f32 -> out complex64 [B][256][Tpad], frames 1 + L/128 (the rest zero).
- * mode 0 raw, 1 exponent transform (|X|^0.5 e^{i angle X} * 0.15).  in_scale multiplies sig. */
-int snrse_stft(const float* sig, int B, int L, float in_scale, int Tpad, int mode, void* out,
-               hipStream_t stream);
+ * mode 0 raw, 1 exponent transform (|X|^0.5 e^{i angle X} * 0.15).  The signal is scaled by
+ * in_scale / in_div[b] (in_div: per-utterance norm factors on the device, or NULL). */
+int snrse_stft(const float* sig, int B, int L, const float* in_div, float in_scale, int Tpad, int mode,
+               void* out, hipStream_t stream);
 
 /* iSTFT (data_module.py:295-297 with spec_back 256-267): spec complex64 [B][256][T] -> out [B][L]
  * f32, times out_scale[b] (NULL = 1).  frames: workspace of B*T*510 floats. */

@@ -30,14 +30,15 @@ SNRSE_DEV void fill_twiddles(float* cs, float* sn) {
 }
 
 // mode: 0 = raw STFT, 1 = exponent transform (e = 0.5, factor 0.15)
-__global__ __launch_bounds__(256) void stft_kernel(const float* sig, int L, float in_scale, int T, int Tpad,
-                                                   int mode, float2* out) {
+__global__ __launch_bounds__(256) void stft_kernel(const float* sig, int L, const float* in_div, float in_scale,
+                                                   int T, int Tpad, int mode, float2* out) {
   __shared__ float cs[NFFT], sn[NFFT];
   __shared__ float xs[(FPB - 1) * HOP + NFFT];
   const int b = blockIdx.y;
   const int f0 = blockIdx.x * FPB;
   fill_twiddles(cs, sn);
   const int span = (FPB - 1) * HOP + NFFT;
+  const float scale = in_div ? in_scale / in_div[b] : in_scale;
   for (int j = threadIdx.x; j < span; j += 256) {
     int s = f0 * HOP + j - NFFT / 2;
     if (s < 0) s = -s;
@@ -45,7 +46,7 @@ __global__ __launch_bounds__(256) void stft_kernel(const float* sig, int L, floa
     // frames >= T (zero padding up to Tpad) read past the reflect range; their output is
     // discarded, clamp the address so the load stays in bounds.
     s = s < 0 ? 0 : (s >= L ? L - 1 : s);
-    xs[j] = sig[(size_t)b * L + s] * in_scale;
+    xs[j] = sig[(size_t)b * L + s] * scale;
   }
   __syncthreads();
   const int k = threadIdx.x;  // bin
@@ -146,14 +147,32 @@ __global__ __launch_bounds__(256) void istft_ola_kernel(const float* frames, int
   out[(size_t)b * L + i] = env > 1e-11f ? y / env * sc : 0.f;
 }
 
+// out[b] = max |sig[b, :]|  (norm_factor = y.abs().max(), model.py:726)
+__global__ __launch_bounds__(256) void absmax_kernel(const float* sig, int L, float* out) {
+  const int b = blockIdx.x;
+  float m = 0.f;
+  for (int i = threadIdx.x; i < L; i += 256) m = fmaxf(m, fabsf(sig[(size_t)b * L + i]));
+  m = wave_max(m);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) out[b] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
 }  // namespace
 
-extern "C" int snrse_stft(const float* sig, int B, int L, float in_scale, int Tpad, int mode, void* out,
-                          hipStream_t s) {
+extern "C" int snrse_absmax(const float* sig, int B, int L, float* out, hipStream_t s) {
+  if (B <= 0 || L <= 0 || !sig || !out) return SNRSE_EINVAL;
+  hipLaunchKernelGGL(absmax_kernel, dim3(B), dim3(256), 0, s, sig, L, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int snrse_stft(const float* sig, int B, int L, const float* in_div, float in_scale, int Tpad, int mode,
+                          void* out, hipStream_t s) {
   const int T = 1 + L / HOP;
   if (B <= 0 || L <= NFFT / 2 || Tpad < T || (mode != 0 && mode != 1)) return SNRSE_EINVAL;
   dim3 grid((Tpad + FPB - 1) / FPB, B);
-  hipLaunchKernelGGL(stft_kernel, grid, dim3(256), 0, s, sig, L, in_scale, T, Tpad, mode, (float2*)out);
+  hipLaunchKernelGGL(stft_kernel, grid, dim3(256), 0, s, sig, L, in_div, in_scale, T, Tpad, mode, (float2*)out);
   return (int)hipGetLastError();
 }
 

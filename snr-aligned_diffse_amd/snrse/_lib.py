@@ -34,7 +34,8 @@ SIGNATURES = {
     "snrse_score_update": [_vp, _i, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp],
     "snrse_sde_update": [_vp, _vp, _vp, _vp, _u64, _u64, _vp, _i, _i, _vp, _vp, _vp],
     "snrse_axpby_noise": [_vp, _vp, _vp, _u64, _u64, _vp, _i, _i, _vp, _vp],
-    "snrse_stft": [_vp, _i, _i, _f, _i, _i, _vp, _vp],
+    "snrse_stft": [_vp, _i, _i, _vp, _f, _i, _i, _vp, _vp],
+    "snrse_absmax": [_vp, _i, _i, _vp, _vp],
     "snrse_istft": [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
 }
 HOUSEKEEPING = {"snrse_abi_version": ([], _i), "snrse_error_string": ([_i], C.c_char_p),

@@ -170,14 +170,24 @@ def axpby_noise(coef, x=None, y=None, noise=None, seed=0, offset=0, like=None):
     return out
 
 
-def stft(sig, in_scale=1.0, tpad=None, mode=1):
-    """sig [B, L] f32 -> complex64 [B, 256, Tpad]."""
+def absmax(sig):
+    """[B, L] f32 -> [B] max |sig| per row."""
     _dev(sig)
+    B, L = sig.shape
+    out = torch.empty(B, device=sig.device, dtype=torch.float32)
+    _lib.call("snrse_absmax", sig.data_ptr(), B, L, out.data_ptr(), _stream())
+    return out
+
+
+def stft(sig, in_scale=1.0, tpad=None, mode=1, in_div=None):
+    """sig [B, L] f32 -> complex64 [B, 256, Tpad] of sig * in_scale / in_div[b]."""
+    _dev(sig, in_div)
     B, L = sig.shape
     T = 1 + L // 128
     tpad = T if tpad is None else tpad
     out = torch.empty(B, 256, tpad, device=sig.device, dtype=torch.complex64)
-    _lib.call("snrse_stft", sig.data_ptr(), B, L, float(in_scale), tpad, int(mode), out.data_ptr(), _stream())
+    _lib.call("snrse_stft", sig.data_ptr(), B, L, _ptr(in_div), float(in_scale), tpad, int(mode), out.data_ptr(),
+              _stream())
     return out
 
 
