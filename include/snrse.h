@@ -49,25 +49,30 @@ int snrse_upfirdn2d(const void* in, void* out, const float* kernel, int major, i
  *   sc_src/sc_src1 (optional): 1x1 shortcut input(s) appended as extra K; sc_wgt [Npad][Csc+Csc1]
  *   out[m][n] = ((acc + bias[n] + temb[b][n] + res[m][n]) * out_scale)
  *               + (comb_src ? comb_src[m][0:4] . comb_w[n][0:4] + comb_b[n] : 0)
- *   out_f32: write float output (bf16 mode pyramid heads); res then is float too. */
+ *   out_f32: write float output (bf16 mode pyramid heads); res then is float too.
+ *   stats (optional): per-channel (sum, sumsq) of out, [B][Cout][2] double, for the next
+ *          GroupNorm (zeroed by the call). */
 int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, int B, int H, int W, int ksize,
                  const void* wgt, const void* sc_src, int Csc, const void* sc_src1, int Csc1,
                  const void* sc_wgt, const float* bias, const float* temb, int temb_stride,
                  const void* res, int res_ld, float out_scale, const float* comb_src,
                  const float* comb_w, const float* comb_b, void* out, int Cout, int out_ld,
-                 int dtype, int out_f32, hipStream_t stream);
+                 double* stats, int dtype, int out_f32, hipStream_t stream);
 
-/* GroupNorm statistics (nn.GroupNorm, layerspp.py:221,233): per-channel (sum, sumsq) of
- * concat(src0, src1) over H*W into sums [B][C0+C1][2] (double; zeroed by the call). */
+/* GroupNorm statistics (nn.GroupNorm, layerspp.py:221,233): per-channel (sum, sumsq) over
+ * H*W of src0 into sums [B][C0][2] and of src1 into sums1 [B][C1][2] (double; zeroed by the call). */
 int snrse_gn_stats(const void* src0, int C0, const void* src1, int C1, int B, int HW, double* sums,
-                   int dtype, hipStream_t stream);
+                   double* sums1, int dtype, hipStream_t stream);
 
 /* Fused GroupNorm-apply (+SiLU) (+FIR [1,3,3,1] down/up x2) (layerspp.py:245-257,
  * up_or_down_sampling.py:195-257).  sums == NULL: identity normalisation (plain FIR of x).
  * mode: 0 none, 1 down (out H/2 x W/2), 2 up (out 2H x 2W).  out [B][Ho][Wo][C0+C1]. */
 int snrse_gn_apply(const void* src0, int C0, const void* src1, int C1, int B, int H, int W,
-                   const double* sums, const float* gamma, const float* beta, int groups, float eps,
-                   int act, int mode, void* out, int dtype, hipStream_t stream);
+                   const double* sums, const double* sums1, const float* gamma, const float* beta,
+                   int groups, float eps, int act, int mode, void* out, int dtype, hipStream_t stream);
+
+/* Tuning switches (A/B experiments): "conv_variant" 0 auto, 1 register-staged v1, 2 LDS-DMA v2. */
+int snrse_set_option(const char* name, int value);
 
 /* AttnBlockpp attention core (layerspp.py:84-88): qkv [B][L][3C] -> out [B][L][C],
  * softmax(q k^T / sqrt(C)) v, flash-style on MFMA.  C must be 256. */

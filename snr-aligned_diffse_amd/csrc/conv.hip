@@ -16,8 +16,9 @@
 //
 // MFMA: v_mfma_f32_16x16x32_bf16 (bf16) / v_mfma_f32_16x16x4_f32 (exact f32 parity mode).
 // Both read one 16-byte LDS chunk per operand fragment with the same swizzled layout:
-// rows of 128 B, chunk' = chunk ^ ((row >> 1) & 7) (conflict-free for the ds_read_b128
-// lane groups of a 16-row fragment).
+// rows of 128 B, chunk' = chunk ^ (row & 7): conflict-free for the ds_read_b128 lane groups
+// of ANY 16 consecutive rows (each group's rows cover all residues mod 8), which the halo
+// kernel needs because its fragments start at arbitrary (tap-shifted) rows.
 #include "common.h"
 
 namespace {
@@ -49,7 +50,10 @@ struct ConvParams {
   const float* comb_w;    // [Cout][4]
   const float* comb_b;    // [Cout]
   void* out; int Cout; int out_ld;
+  double* stats;  // optional [B][Cout][2] per-channel (sum, sumsq) of the output (zeroed by launcher)
   int M;
+  int ntn;        // N tiles (v2 grid)
+  long long bytes0, bytes1, sc_bytes0, sc_bytes1, wbytes, sc_wbytes;  // buffer extents (v2)
 };
 
 template <typename T>
@@ -69,7 +73,76 @@ SNRSE_DEV f32x4 mfma_chunk<float>(const u32x4& a, const u32x4& b, f32x4 acc) {
   return acc;
 }
 
-SNRSE_DEV int swz(int row, int chunk) { return (row << 7) + ((chunk ^ ((row >> 1) & 7)) << 4); }
+SNRSE_DEV int swz(int row, int chunk) { return (row << 7) + ((chunk ^ (row & 7)) << 4); }
+
+SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
+}
+
+// Shared epilogue: y = (acc + bias + temb + res) * out_scale + combine; optional GroupNorm
+// statistics of y (per (b, channel) sum / sumsq) for the consumer's GroupNorm.
+// acc[i][j][e]: row = mb + i*16 + (lane>>4)*4 + e, col = nb + j*16 + (lane&15).
+template <typename TO, int FM, int FN>
+SNRSE_DEV void epilogue(const ConvParams& p, const f32x4 (&acc)[FM][FN], int mb, int nb, int lane) {
+  const int lrow = lane & 15, lg = lane >> 4;
+  const int HW = p.H * p.W;
+  const int m_last = min(mb + FM * 16, p.M) - 1;
+  const bool one_b = mb < p.M && (mb / HW) == (m_last / HW);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = nb + j * 16 + lrow;
+    const bool nok = n < p.Cout;
+    const float bn = (p.bias && nok) ? p.bias[n] : 0.f;
+    float cw0 = 0.f, cw1 = 0.f, cw2 = 0.f, cw3 = 0.f, cb = 0.f;
+    if (p.comb_src && nok) {
+      cw0 = p.comb_w[n * 4 + 0]; cw1 = p.comb_w[n * 4 + 1];
+      cw2 = p.comb_w[n * 4 + 2]; cw3 = p.comb_w[n * 4 + 3];
+      cb = p.comb_b[n];
+    }
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = mb + i * 16 + lg * 4 + e;
+        if (m >= p.M || !nok) continue;
+        float v = acc[i][j][e] + bn;
+        if (p.temb) v += p.temb[(size_t)(m / HW) * p.temb_stride + n];
+        if (p.res) v += Elem<TO>::to_f(((const TO*)p.res)[(size_t)m * p.res_ld + n]);
+        v *= p.out_scale;
+        if (p.comb_src) {
+          const float* q = p.comb_src + (size_t)m * 4;
+          v += q[0] * cw0 + q[1] * cw1 + q[2] * cw2 + q[3] * cw3 + cb;
+        }
+        ((TO*)p.out)[(size_t)m * p.out_ld + n] = Elem<TO>::from_f(v);
+        if (p.stats) {
+          if (one_b) {
+            s1 += v;
+            s2 = fmaf(v, v, s2);
+          } else {
+            unsafeAtomicAdd(&p.stats[((size_t)(m / HW) * p.Cout + n) * 2], (double)v);
+            unsafeAtomicAdd(&p.stats[((size_t)(m / HW) * p.Cout + n) * 2 + 1], (double)v * v);
+          }
+        }
+      }
+    }
+    if (p.stats && one_b) {
+      s1 += __shfl_xor(s1, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (lg == 0 && nok) {
+        const size_t o = ((size_t)(mb / HW) * p.Cout + n) * 2;
+        unsafeAtomicAdd(&p.stats[o], (double)s1);
+        unsafeAtomicAdd(&p.stats[o + 1], (double)s2);
+      }
+    }
+  }
+}
 
 template <typename T, typename TO, int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(64 * WM * WN) void conv_mfma_kernel(ConvParams p) {
@@ -91,8 +164,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma_kernel(ConvParams p) {
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  const int nbk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nbk >> 3, r8 = nbk & 7, xcd = bid & 7, pos = bid >> 3;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
+  const int m0 = (wg / p.ntn) * BM;
+  const int n0 = (wg % p.ntn) * BN;
   const int HW = p.H * p.W;
   const int Cin = p.C0 + p.C1;
   const int cblocks = Cin / Tr::KT;
@@ -208,50 +284,379 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma_kernel(ConvParams p) {
 
 #undef AS
 #undef BS
-  // epilogue
+  epilogue<TO, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, lane);
+}
+
+// ---------------------------------------------------------------------------------------
+// v2 (bf16): 8 waves, 64x64 wave tiles, operands streamed global->LDS by buffer_load...lds
+// (LDS-DMA, no VGPR staging), 3-stage ring with counted vmcnt + raw s_barrier so two
+// K-tiles stay in flight across the barrier.  Zero padding of the 3x3 halo comes from the
+// buffer's range check (an out-of-range voffset loads 0).  The LDS image is lane-linear per
+// DMA instruction; the chunk swizzle is applied to the per-lane SOURCE address and the
+// same XOR on the ds_read (conflict-free 16-row fragment reads).
+template <int BM, int BN, typename TO>
+__global__ __launch_bounds__(512) void conv_glds_kernel(ConvParams p) {
+  constexpr int WM = BM / 64, WN = BN / 64;
+  static_assert(WM * WN == 8, "8 waves");
+  constexpr int FM = 4, FN = 4, TM = 64, TN = 64;
+  constexpr int STAGES = 3;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int AJ = BM / 64, BJ = BN / 64;  // DMA instructions per wave per stage
+  constexpr int KT = 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  // XCD-aware bijective remap: consecutive logical tiles share an XCD (its L2 holds the halo
+  // rows and the weight tile they all re-read); N-tiles of one M-tile are adjacent.
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7, pos = bid >> 3;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
+  const int m0 = (wg / p.ntn) * BM;
+  const int n0 = (wg % p.ntn) * BN;
+
+  const int HW = p.H * p.W;
+  const int Cin = p.C0 + p.C1;
+  const int cblocks = Cin / KT;
+  const int nk0 = p.ksize * p.ksize * cblocks;
+  const int Csc_all = p.Csc + p.Csc1;
+  const int nk = nk0 + (p.sc_src ? Csc_all / KT : 0);
+  const int K1 = p.ksize * p.ksize * Cin;
+  const int half = p.ksize >> 1;
+  const int slot = lane & 7;
+
+  int a_pix[AJ], a_h[AJ], a_w[AJ], a_ch[AJ];
+  bool a_ok[AJ];
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int n = n0 + wn * TN + j * 16 + lrow;
-    if (n >= p.Cout) continue;
-    const float bn = p.bias ? p.bias[n] : 0.f;
-    float cw0 = 0.f, cw1 = 0.f, cw2 = 0.f, cw3 = 0.f, cb = 0.f;
-    if (p.comb_src) {
-      cw0 = p.comb_w[n * 4 + 0]; cw1 = p.comb_w[n * 4 + 1];
-      cw2 = p.comb_w[n * 4 + 2]; cw3 = p.comb_w[n * 4 + 3];
-      cb = p.comb_b[n];
-    }
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = m0 + wm * TM + i * 16 + lg * 4 + e;
-        if (m >= p.M) continue;
-        float v = acc[i][j][e] + bn;
-        if (p.temb) v += p.temb[(size_t)(m / HW) * p.temb_stride + n];
-        if (p.res) v += Elem<TO>::to_f(((const TO*)p.res)[(size_t)m * p.res_ld + n]);
-        v *= p.out_scale;
-        if (p.comb_src) {
-          const float* q = p.comb_src + (size_t)m * 4;
-          v += q[0] * cw0 + q[1] * cw1 + q[2] * cw2 + q[3] * cw3 + cb;
-        }
-        ((TO*)p.out)[(size_t)m * p.out_ld + n] = Elem<TO>::from_f(v);
-      }
-    }
+  for (int j = 0; j < AJ; ++j) {
+    const int row = (wid * AJ + j) * 8 + (lane >> 3);
+    const int m = m0 + row;
+    a_ok[j] = m < p.M;
+    const int mm = a_ok[j] ? m : 0;
+    const int b = mm / HW, rem = mm - b * HW;
+    a_h[j] = rem / p.W;
+    a_w[j] = rem - a_h[j] * p.W;
+    a_pix[j] = mm;
+    a_ch[j] = slot ^ (row & 7);
   }
+
+  // one K-tile -> one LDS stage.  Every selector below depends only on kt (wave-uniform),
+  // and the buffer base / extent go through readfirstlane so the descriptor lives in SGPRs
+  // (no waterfall loop around the DMA, guide T20).
+#define SNRSE_ISSUE(KT_, STAGE_)                                                                      \
+  do {                                                                                              \
+    const int kt_ = (KT_);                                                                          \
+    char* sa_ = smem + (STAGE_) * STAGE;                                                            \
+    char* sb_ = sa_ + A_BYTES;                                                                      \
+    int cs_, cc_, dy_, dx_, wld_, koff_;                                                            \
+    const void* abase_;                                                                             \
+    long long abytes_;                                                                              \
+    const void* wbase_;                                                                             \
+    long long wbytes_;                                                                              \
+    if (kt_ < nk0) {                                                                                \
+      const int tap_ = kt_ / cblocks;                                                               \
+      const int c_ = (kt_ - tap_ * cblocks) * KT;                                                   \
+      dy_ = tap_ / p.ksize - half;                                                                  \
+      dx_ = tap_ - (tap_ / p.ksize) * p.ksize - half;                                               \
+      const bool u1_ = c_ >= p.C0;                                                                  \
+      abase_ = u1_ ? p.src1 : p.src0;                                                               \
+      abytes_ = u1_ ? p.bytes1 : p.bytes0;                                                          \
+      cs_ = u1_ ? p.C1 : p.C0;                                                                      \
+      cc_ = u1_ ? c_ - p.C0 : c_;                                                                   \
+      wbase_ = p.wgt;                                                                               \
+      wbytes_ = p.wbytes;                                                                           \
+      wld_ = K1;                                                                                    \
+      koff_ = tap_ * Cin + c_;                                                                      \
+    } else {                                                                                        \
+      const int c_ = (kt_ - nk0) * KT;                                                              \
+      const bool u1_ = c_ >= p.Csc;                                                                 \
+      abase_ = u1_ ? p.sc_src1 : p.sc_src;                                                          \
+      abytes_ = u1_ ? p.sc_bytes1 : p.sc_bytes0;                                                    \
+      cs_ = u1_ ? p.Csc1 : p.Csc;                                                                   \
+      cc_ = u1_ ? c_ - p.Csc : c_;                                                                  \
+      dy_ = 0;                                                                                      \
+      dx_ = 0;                                                                                      \
+      wbase_ = p.sc_wgt;                                                                            \
+      wbytes_ = p.sc_wbytes;                                                                        \
+      wld_ = Csc_all;                                                                               \
+      koff_ = c_;                                                                                   \
+    }                                                                                               \
+    const __amdgpu_buffer_rsrc_t ra_ = make_rsrc(abase_, abytes_);                                  \
+    const __amdgpu_buffer_rsrc_t rb_ = make_rsrc(wbase_, wbytes_);                                  \
+    const int shift_ = dy_ * p.W + dx_;                                                             \
+    _Pragma("unroll") for (int j = 0; j < AJ; ++j) {                                                \
+      const int hh_ = a_h[j] + dy_, ww_ = a_w[j] + dx_;                                             \
+      const bool ok_ = a_ok[j] && hh_ >= 0 && hh_ < p.H && ww_ >= 0 && ww_ < p.W;                   \
+      const unsigned voff_ =                                                                        \
+          ok_ ? (unsigned)(((a_pix[j] + shift_) * cs_ + cc_ + a_ch[j] * 8) * 2) : 0x80000000u;      \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                     \
+          ra_, (__attribute__((address_space(3))) void*)(sa_ + (wid * AJ + j) * 1024), 16, voff_, 0, 0, 0); \
+    }                                                                                               \
+    _Pragma("unroll") for (int j = 0; j < BJ; ++j) {                                                \
+      const int row_ = (wid * BJ + j) * 8 + (lane >> 3);                                            \
+      const int chk_ = slot ^ (row_ & 7);                                                           \
+      const unsigned voff_ = (unsigned)(((n0 + row_) * wld_ + koff_ + chk_ * 8) * 2);               \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                     \
+          rb_, (__attribute__((address_space(3))) void*)(sb_ + (wid * BJ + j) * 1024), 16, voff_, 0, 0, 0); \
+    }                                                                                               \
+  } while (0)
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  SNRSE_ISSUE(0, 0);
+  if (nk > 1) SNRSE_ISSUE(1, 1);
+  const int lrow = lane & 15, lg = lane >> 4;
+  int stage = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AJ + BJ) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) SNRSE_ISSUE(kt + 2, stage == 0 ? 2 : stage - 1);
+    const char* sa = smem + stage * STAGE;
+    const char* sb = sa + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      u32x4 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *(const u32x4*)(sa + swz(wm * TM + i * 16 + lrow, 4 * s + lg));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = *(const u32x4*)(sb + swz(wn * TN + j * 16 + lrow, 4 * s + lg));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<bf16_t>(af[i], bfr[j], acc[i][j]);
+    }
+    stage = stage == STAGES - 1 ? 0 : stage + 1;
+  }
+#undef SNRSE_ISSUE
+  epilogue<TO, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, lane);
+}
+
+// ---------------------------------------------------------------------------------------
+// v3 (bf16, 3x3, H % 4 == 0, W % 64 == 0): halo tiles.  Output tile = 4 frequency rows x 64
+// frames (256 pixels) x 128 output channels.  Per 64-channel block the (4+2) x (64+2) input
+// halo is DMA'd into LDS once and all 9 taps read their A fragments from it at shifted rows
+// (the row&7 swizzle keeps every 16-row read conflict-free), so an input element crosses
+// L2 -> LDS ~1.5x per conv instead of 9x (v2).  Weight tiles (tap, channel block) stream
+// through a 3-slot ring two steps ahead.  The 1x1 shortcut K-blocks reuse the halo path
+// with the center tap only.  LDS: 2 x 56 KiB halo + 3 x 16 KiB weights = 160 KiB.
+template <typename TO>
+__global__ __launch_bounds__(512) void conv_halo_kernel(ConvParams p) {
+  constexpr int TH = 4, TW = 64, HC = TW + 2;
+  constexpr int HROWS = (TH + 2) * HC;       // 396
+  constexpr int HJ = 7;                      // DMA instructions per wave per halo (448 rows)
+  constexpr int HALO_BYTES = 8 * HJ * 1024;  // 57344
+  constexpr int BJ = 2, B_BYTES = 128 * 128;
+  constexpr int FM = 4, FN = 4, KT = 64;
+  static_assert(8 * HJ * 8 >= HROWS, "halo rows");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const halo0 = smem;
+  char* const bring = smem + 2 * HALO_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7, pos = bid >> 3;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
+  const int n0 = (wg % p.ntn) * 128;
+  int tile = wg / p.ntn;
+  const int ntw = p.W / TW, nth = p.H / TH;
+  const int w0 = (tile % ntw) * TW;
+  tile /= ntw;
+  const int h0 = (tile % nth) * TH;
+  const int bb = tile / nth;
+
+  const int Cin = p.C0 + p.C1;
+  const int cbm = Cin / KT;
+  const int Csc_all = p.Csc + p.Csc1;
+  const int cbs = p.sc_src ? Csc_all / KT : 0;
+  const int ncb = cbm + cbs;
+  const int S = 9 * cbm + cbs;
+  const int K1 = 9 * Cin;
+  const int slot = lane & 7;
+
+  int hpix[HJ], hch[HJ];
+  bool hok[HJ];
+#pragma unroll
+  for (int j = 0; j < HJ; ++j) {
+    const int hr = (wid * HJ + j) * 8 + (lane >> 3);
+    const int hy = hr / HC, hx = hr - (hr / HC) * HC;
+    const int ih = h0 + hy - 1, iw = w0 + hx - 1;
+    hok[j] = hr < HROWS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+    hpix[j] = (bb * p.H + ih) * p.W + iw;
+    hch[j] = slot ^ (hr & 7);
+  }
+
+  auto step_cb = [](int s_, int cbm_) { return s_ < 9 * cbm_ ? s_ / 9 : cbm_ + (s_ - 9 * cbm_); };
+  auto step_tap = [](int s_, int cbm_) { return s_ < 9 * cbm_ ? s_ % 9 : 4; };
+
+#define SNRSE_HALO(CB_)                                                                               \
+  do {                                                                                              \
+    const int c_ = (CB_);                                                                           \
+    const void* base_;                                                                              \
+    long long bytes_;                                                                               \
+    int cs_, cc_;                                                                                   \
+    if (c_ < cbm) {                                                                                 \
+      const int ch_ = c_ * KT;                                                                      \
+      const bool u1_ = ch_ >= p.C0;                                                                 \
+      base_ = u1_ ? p.src1 : p.src0;                                                                \
+      bytes_ = u1_ ? p.bytes1 : p.bytes0;                                                           \
+      cs_ = u1_ ? p.C1 : p.C0;                                                                      \
+      cc_ = u1_ ? ch_ - p.C0 : ch_;                                                                 \
+    } else {                                                                                        \
+      const int ch_ = (c_ - cbm) * KT;                                                              \
+      const bool u1_ = ch_ >= p.Csc;                                                                \
+      base_ = u1_ ? p.sc_src1 : p.sc_src;                                                           \
+      bytes_ = u1_ ? p.sc_bytes1 : p.sc_bytes0;                                                     \
+      cs_ = u1_ ? p.Csc1 : p.Csc;                                                                   \
+      cc_ = u1_ ? ch_ - p.Csc : ch_;                                                                \
+    }                                                                                               \
+    const __amdgpu_buffer_rsrc_t r_ = make_rsrc(base_, bytes_);                                     \
+    char* dst_ = halo0 + (c_ & 1) * HALO_BYTES;                                                     \
+    _Pragma("unroll") for (int j = 0; j < HJ; ++j) {                                                \
+      const unsigned voff_ = hok[j] ? (unsigned)((hpix[j] * cs_ + cc_ + hch[j] * 8) * 2) : 0x80000000u; \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                     \
+          r_, (__attribute__((address_space(3))) void*)(dst_ + (wid * HJ + j) * 1024), 16, voff_, 0, 0, 0); \
+    }                                                                                               \
+  } while (0)
+
+#define SNRSE_WTILE(S_)                                                                               \
+  do {                                                                                              \
+    const int s_ = (S_);                                                                            \
+    const int c_ = step_cb(s_, cbm), t_ = step_tap(s_, cbm);                                        \
+    const void* wb_;                                                                                \
+    long long wbytes_;                                                                              \
+    int wld_, koff_;                                                                                \
+    if (c_ < cbm) { wb_ = p.wgt; wbytes_ = p.wbytes; wld_ = K1; koff_ = t_ * Cin + c_ * KT; }       \
+    else { wb_ = p.sc_wgt; wbytes_ = p.sc_wbytes; wld_ = Csc_all; koff_ = (c_ - cbm) * KT; }        \
+    const __amdgpu_buffer_rsrc_t r_ = make_rsrc(wb_, wbytes_);                                      \
+    char* dst_ = bring + (s_ % 3) * B_BYTES;                                                        \
+    _Pragma("unroll") for (int j = 0; j < BJ; ++j) {                                                \
+      const int row_ = (wid * BJ + j) * 8 + (lane >> 3);                                            \
+      const unsigned voff_ = (unsigned)(((n0 + row_) * wld_ + koff_ + (slot ^ (row_ & 7)) * 8) * 2); \
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                     \
+          r_, (__attribute__((address_space(3))) void*)(dst_ + (wid * BJ + j) * 1024), 16, voff_, 0, 0, 0); \
+    }                                                                                               \
+  } while (0)
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  SNRSE_HALO(0);
+  SNRSE_WTILE(0);
+  if (S > 1) SNRSE_WTILE(1);
+  const int lrow = lane & 15, lg = lane >> 4;
+  int prev_halo_cb = -1;  // cb whose halo was issued in the previous step (-1: none)
+  int c = 0, t = 0;       // cb / tap of the current step
+  for (int s = 0; s < S; ++s) {
+    // wait: everything but the previous step's issues, unless that step issued this cb's halo
+    if (s == 0) {
+      if (S > 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (prev_halo_cb == c || s + 1 >= S) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (prev_halo_cb >= 0) {
+      asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const int ntap = c < cbm ? 9 : 1;
+    if (s + 2 < S) SNRSE_WTILE(s + 2);
+    prev_halo_cb = -1;
+    if (c + 1 < ncb && t == (ntap >= 5 ? 4 : 0)) {
+      SNRSE_HALO(c + 1);
+      prev_halo_cb = c + 1;
+    }
+    const int tp = c < cbm ? t : 4;
+    const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
+    const char* ha = halo0 + (c & 1) * HALO_BYTES;
+    const char* sb = bring + (s % 3) * B_BYTES;
+    const int hbase = (wm + dy + 1) * HC + dx + 1 + lrow;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      u32x4 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = *(const u32x4*)(ha + swz(hbase + i * 16, 4 * k + lg));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = *(const u32x4*)(sb + swz(wn * 64 + j * 16 + lrow, 4 * k + lg));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<bf16_t>(af[i], bfr[j], acc[i][j]);
+    }
+    if (++t == ntap) { t = 0; ++c; }
+  }
+#undef SNRSE_HALO
+#undef SNRSE_WTILE
+  epilogue<TO, FM, FN>(p, acc, (bb * p.H + h0 + wm) * p.W + w0, n0 + wn * 64, lane);
+}
+
+template <typename TO>
+int launch_halo(ConvParams p, hipStream_t s) {
+  constexpr size_t lds = 2 * 8 * 7 * 1024 + 3 * 128 * 128;
+  static bool attr = false;
+  if (!attr) {
+    SNRSE_RET(hipFuncSetAttribute((const void*)conv_halo_kernel<TO>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+    attr = true;
+  }
+  p.ntn = p.Cout / 128;
+  const int tiles = p.B * (p.H / 4) * (p.W / 64);
+  hipLaunchKernelGGL((conv_halo_kernel<TO>), dim3(tiles * p.ntn), dim3(512), lds, s, p);
+  return (int)hipGetLastError();
 }
 
 template <typename T, typename TO, int BM, int BN, int WM, int WN>
-int launch_conv(const ConvParams& p, int npad, hipStream_t s) {
-  dim3 grid((p.M + BM - 1) / BM, npad / BN);
+int launch_conv(ConvParams p, int npad, hipStream_t s) {
+  p.ntn = npad / BN;
+  dim3 grid(((p.M + BM - 1) / BM) * p.ntn);
   const size_t lds = (size_t)2 * (BM + BN) * 128;
   hipLaunchKernelGGL((conv_mfma_kernel<T, TO, BM, BN, WM, WN>), grid, dim3(64 * WM * WN), lds, s, p);
   return (int)hipGetLastError();
 }
 
+template <int BM, int BN, typename TO>
+int launch_glds(ConvParams p, hipStream_t s) {
+  constexpr size_t lds = (size_t)3 * (BM + BN) * 128;
+  static bool attr = false;
+  if (!attr) {
+    SNRSE_RET(hipFuncSetAttribute((const void*)conv_glds_kernel<BM, BN, TO>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  p.ntn = p.Cout / BN;
+  const int ntm = (p.M + BM - 1) / BM;
+  hipLaunchKernelGGL((conv_glds_kernel<BM, BN, TO>), dim3(ntm * p.ntn), dim3(512), lds, s, p);
+  return (int)hipGetLastError();
+}
+
+int g_conv_variant = 0;  // 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 3 = auto
+
 template <typename T, typename TO>
 int dispatch_conv(const ConvParams& p, hipStream_t s) {
   if (p.Cout >= 64) {
     if (p.Cout % 128 != 0) return SNRSE_EINVAL;
+    if constexpr (sizeof(T) == 2) {
+      const bool fits = p.bytes0 < 0x7ff00000ll && p.bytes1 < 0x7ff00000ll && p.sc_bytes0 < 0x7ff00000ll &&
+                        p.sc_bytes1 < 0x7ff00000ll;
+      if (g_conv_variant != 1 && fits) {
+        if (g_conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0) return launch_halo<TO>(p, s);
+        if (p.Cout % 256 == 0) return launch_glds<128, 256, TO>(p, s);
+        return launch_glds<256, 128, TO>(p, s);
+      }
+    }
     return launch_conv<T, TO, 128, 128, 2, 2>(p, p.Cout, s);
   }
   if (p.Cout > 16) return SNRSE_EINVAL;
@@ -265,8 +670,8 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
                             int Csc1, const void* sc_wgt,
                             const float* bias, const float* temb, int temb_stride, const void* res,
                             int res_ld, float out_scale, const float* comb_src, const float* comb_w,
-                            const float* comb_b, void* out, int Cout, int out_ld, int dtype,
-                            int out_f32, hipStream_t stream) {
+                            const float* comb_b, void* out, int Cout, int out_ld, double* stats,
+                            int dtype, int out_f32, hipStream_t stream) {
   using TrB = ConvTraits<bf16_t>;
   using TrF = ConvTraits<float>;
   const int KT = dtype == SNRSE_BF16 ? TrB::KT : TrF::KT;
@@ -283,10 +688,32 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
   p.res = res; p.res_ld = res_ld; p.out_scale = out_scale;
   p.comb_src = comb_src; p.comb_w = comb_w; p.comb_b = comb_b;
   p.out = out; p.Cout = Cout; p.out_ld = out_ld; p.M = B * H * W;
+  p.stats = stats;
   if (p.M <= 0) return 0;
+  const long long esz = dtype == SNRSE_BF16 ? 2 : 4;
+  const long long pix = (long long)B * H * W;
+  p.bytes0 = pix * C0 * esz; p.bytes1 = pix * C1 * esz;
+  p.sc_bytes0 = pix * p.Csc * esz; p.sc_bytes1 = pix * p.Csc1 * esz;
+  const int npad = Cout >= 64 ? Cout : 16;
+  p.wbytes = (long long)npad * ksize * ksize * (C0 + C1) * esz;
+  p.sc_wbytes = (long long)npad * (p.Csc + p.Csc1) * esz;
+  p.ntn = 1;
+  if (stats) SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * (size_t)B * Cout, stream));
   if (dtype == SNRSE_BF16) {
     return out_f32 ? dispatch_conv<bf16_t, float>(p, stream) : dispatch_conv<bf16_t, bf16_t>(p, stream);
   }
   if (dtype == SNRSE_F32) return dispatch_conv<float, float>(p, stream);
+  return SNRSE_EINVAL;
+}
+
+extern "C" int snrse_set_option(const char* name, int value) {
+  if (!name) return SNRSE_EINVAL;
+  const char* k = "conv_variant";
+  int i = 0;
+  while (k[i] && name[i] == k[i]) ++i;
+  if (k[i] == 0 && name[i] == 0) {
+    g_conv_variant = value;
+    return 0;
+  }
   return SNRSE_EINVAL;
 }

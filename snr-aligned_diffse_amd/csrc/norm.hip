@@ -48,10 +48,10 @@ SNRSE_DEV void store_vec(T* p, const float* v) {
   *(u32x4*)p = r;
 }
 
-// grid (nblk, B), block 256.  sums: [B][C][2] double, zeroed by the launcher.
+// grid (nblk, B), block 256.  sums0 [B][C0][2], sums1 [B][C1][2] double, zeroed by the launcher.
 template <typename T>
 __global__ __launch_bounds__(256) void gn_stats_kernel(const T* src0, int C0, const T* src1, int C1,
-                                                       int HW, int pix_per_blk, double* sums) {
+                                                       int HW, int pix_per_blk, double* sums0, double* sums1) {
   constexpr int V = VecT<T>::N;
   const int C = C0 + C1;
   const int LP = C / V;        // vectors per pixel
@@ -85,7 +85,11 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const T* src0, int C0, co
     }
   }
   __syncthreads();
-  for (int i = tid; i < 2 * C; i += 256) atomicAdd(&sums[(size_t)b * 2 * C + i], (double)red[i]);
+  for (int i = tid; i < 2 * C; i += 256) {
+    const int c = i >> 1;
+    if (c < C0) unsafeAtomicAdd(&sums0[((size_t)b * C0 + c) * 2 + (i & 1)], (double)red[i]);
+    else unsafeAtomicAdd(&sums1[((size_t)b * C1 + c - C0) * 2 + (i & 1)], (double)red[i]);
+  }
 }
 
 enum { MODE_NONE = 0, MODE_DOWN = 1, MODE_UP = 2 };
@@ -95,7 +99,8 @@ enum { MODE_NONE = 0, MODE_DOWN = 1, MODE_UP = 2 };
 template <typename Tin, typename Tout, int MODE>
 __global__ __launch_bounds__(256) void gn_apply_kernel(const Tin* src0, int C0, const Tin* src1, int C1,
                                                        int H, int W, const double* sums,
-                                                       const float* gamma, const float* beta, int groups,
+                                                       const double* sums1, const float* gamma,
+                                                       const float* beta, int groups,
                                                        float eps, int act, Tout* out, int opix_per_blk) {
   constexpr int V = VecT<Tin>::N;
   static_assert(VecT<Tin>::N == VecT<Tout>::N || sizeof(Tout) == 4, "vec");
@@ -110,8 +115,9 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const Tin* src0, int C0, 
       const int g = c / cg;
       double s = 0.0, ss = 0.0;
       for (int k = g * cg; k < (g + 1) * cg; ++k) {
-        s += sums[((size_t)b * C + k) * 2];
-        ss += sums[((size_t)b * C + k) * 2 + 1];
+        const double* q = k < C0 ? sums + ((size_t)b * C0 + k) * 2 : sums1 + ((size_t)b * C1 + k - C0) * 2;
+        s += q[0];
+        ss += q[1];
       }
       const double mean = s / cnt;
       double var = ss / cnt - mean * mean;
@@ -221,11 +227,12 @@ __global__ void upfirdn2d_kernel(const T* in, T* out, const float* kern, int maj
 }  // namespace
 
 extern "C" int snrse_gn_stats(const void* src0, int C0, const void* src1, int C1, int B, int HW,
-                              double* sums, int dtype, hipStream_t stream) {
+                              double* sums, double* sums1, int dtype, hipStream_t stream) {
   const int V = dtype == SNRSE_BF16 ? 8 : 4;
   const int C = C0 + C1;
-  if (C % V || C0 % V || C / V > 256 || !sums) return SNRSE_EINVAL;
-  SNRSE_RET(hipMemsetAsync(sums, 0, sizeof(double) * 2 * C * B, stream));
+  if (C % V || C0 % V || C / V > 256 || !sums || (C1 > 0 && !sums1)) return SNRSE_EINVAL;
+  SNRSE_RET(hipMemsetAsync(sums, 0, sizeof(double) * 2 * C0 * B, stream));
+  if (C1 > 0) SNRSE_RET(hipMemsetAsync(sums1, 0, sizeof(double) * 2 * C1 * B, stream));
   int nblk = (HW + 1023) / 1024;
   if (nblk > 256) nblk = 256;
   const int ppb = (HW + nblk - 1) / nblk;
@@ -233,10 +240,10 @@ extern "C" int snrse_gn_stats(const void* src0, int C0, const void* src1, int C1
   const size_t lds = sizeof(float) * 2 * C;
   if (dtype == SNRSE_BF16)
     hipLaunchKernelGGL(gn_stats_kernel<bf16_t>, grid, dim3(256), lds, stream, (const bf16_t*)src0, C0,
-                       (const bf16_t*)src1, C1, HW, ppb, sums);
+                       (const bf16_t*)src1, C1, HW, ppb, sums, sums1);
   else if (dtype == SNRSE_F32)
     hipLaunchKernelGGL(gn_stats_kernel<float>, grid, dim3(256), lds, stream, (const float*)src0, C0,
-                       (const float*)src1, C1, HW, ppb, sums);
+                       (const float*)src1, C1, HW, ppb, sums, sums1);
   else
     return SNRSE_EINVAL;
   return (int)hipGetLastError();
@@ -244,7 +251,7 @@ extern "C" int snrse_gn_stats(const void* src0, int C0, const void* src1, int C1
 
 template <typename Tin, typename Tout>
 static int launch_apply(const void* src0, int C0, const void* src1, int C1, int B, int H, int W,
-                        const double* sums, const float* gamma, const float* beta, int groups, float eps,
+                        const double* sums, const double* sums1, const float* gamma, const float* beta, int groups, float eps,
                         int act, int mode, void* out, hipStream_t stream) {
   const int C = C0 + C1;
   const int Ho = mode == MODE_DOWN ? H / 2 : (mode == MODE_UP ? 2 * H : H);
@@ -257,7 +264,7 @@ static int launch_apply(const void* src0, int C0, const void* src1, int C1, int 
   const size_t lds = sizeof(float) * 2 * C;
 #define SNRSE_APPLY(MODE_)                                                                          \
   hipLaunchKernelGGL((gn_apply_kernel<Tin, Tout, MODE_>), grid, dim3(256), lds, stream, (const Tin*)src0, \
-                     C0, (const Tin*)src1, C1, H, W, sums, gamma, beta, groups, eps, act, (Tout*)out, opb)
+                     C0, (const Tin*)src1, C1, H, W, sums, sums1, gamma, beta, groups, eps, act, (Tout*)out, opb)
   if (mode == MODE_NONE) SNRSE_APPLY(MODE_NONE);
   else if (mode == MODE_DOWN) SNRSE_APPLY(MODE_DOWN);
   else if (mode == MODE_UP) SNRSE_APPLY(MODE_UP);
@@ -267,17 +274,18 @@ static int launch_apply(const void* src0, int C0, const void* src1, int C1, int 
 }
 
 extern "C" int snrse_gn_apply(const void* src0, int C0, const void* src1, int C1, int B, int H, int W,
-                              const double* sums, const float* gamma, const float* beta, int groups,
+                              const double* sums, const double* sums1, const float* gamma, const float* beta,
+                              int groups,
                               float eps, int act, int mode, void* out, int dtype, hipStream_t stream) {
   const int V = dtype == SNRSE_BF16 ? 8 : 4;
   if ((C0 + C1) % V || C0 % V) return SNRSE_EINVAL;
-  if (sums && (!gamma || !beta || groups <= 0 || (C0 + C1) % groups)) return SNRSE_EINVAL;
+  if (sums && (!gamma || !beta || groups <= 0 || (C0 + C1) % groups || (C1 > 0 && !sums1))) return SNRSE_EINVAL;
   if (mode == MODE_DOWN && ((H & 1) || (W & 1))) return SNRSE_EINVAL;
   if (dtype == SNRSE_BF16)
-    return launch_apply<bf16_t, bf16_t>(src0, C0, src1, C1, B, H, W, sums, gamma, beta, groups, eps, act,
+    return launch_apply<bf16_t, bf16_t>(src0, C0, src1, C1, B, H, W, sums, sums1, gamma, beta, groups, eps, act,
                                         mode, out, stream);
   if (dtype == SNRSE_F32)
-    return launch_apply<float, float>(src0, C0, src1, C1, B, H, W, sums, gamma, beta, groups, eps, act,
+    return launch_apply<float, float>(src0, C0, src1, C1, B, H, W, sums, sums1, gamma, beta, groups, eps, act,
                                       mode, out, stream);
   return SNRSE_EINVAL;
 }

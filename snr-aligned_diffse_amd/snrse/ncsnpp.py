@@ -158,38 +158,46 @@ class NCSNppHIP:
         W["dense_b"] = torch.cat(dense_b, 0).contiguous()
 
     # ------------------------------------------------------------------ blocks
+    # Every activation travels with its per-channel GroupNorm statistics, produced by the
+    # epilogue of the GEMM that wrote it, so no separate statistics pass is needed.
+    def _conv(self, *a, **kw):
+        out_stats = kw.pop("want_stats", True)
+        src0 = a[0]
+        st = ops.new_stats(src0.shape[0], a[3]) if out_stats else None
+        out = ops.conv2d(*a, stats=st, **kw)
+        return out, st
+
     def _resblock(self, m, x0, x1, dense, comb=None, comb_w=None, comb_b=None):
+        """x0/x1: (tensor, stats) of the (possibly concatenated) input."""
         e = self.mw[m.idx]
         mode = "up" if m.up else ("down" if m.down else "none")
-        s0 = ops.gn_stats(x0, x1)
-        a0 = ops.gn_apply(x0, x1, s0, e["gn0_g"], e["gn0_b"], act=True, mode=mode)
-        h = ops.conv2d(a0, e["w0"], 3, m.cout, bias=e["b0"], temb=dense, temb_off=e["temb_off"])
-        s1 = ops.gn_stats(h)
-        a1 = ops.gn_apply(h, None, s1, e["gn1_g"], e["gn1_b"], act=True)
+        (t0, s0), (t1, s1) = x0, (x1 if x1 is not None else (None, None))
+        a0 = ops.gn_apply(t0, t1, s0, e["gn0_g"], e["gn0_b"], act=True, mode=mode, sums1=s1)
+        h, hs_ = self._conv(a0, e["w0"], 3, m.cout, bias=e["b0"], temb=dense, temb_off=e["temb_off"])
+        a1 = ops.gn_apply(h, None, hs_, e["gn1_g"], e["gn1_b"], act=True)
         if "w2" in e:
             if mode != "none":
-                xs0, xs1 = ops.fir(x0 if x1 is None else torch.cat([x0, x1], 3), mode), None
+                xs0, xs1 = ops.fir(t0, mode), None
             else:
-                xs0, xs1 = x0, x1
-            return ops.conv2d(a1, e["w1"], 3, m.cout, bias=e["b1"], sc=xs0, sc1=xs1, sc_wgt=e["w2"],
+                xs0, xs1 = t0, t1
+            return self._conv(a1, e["w1"], 3, m.cout, bias=e["b1"], sc=xs0, sc1=xs1, sc_wgt=e["w2"],
                               out_scale=INV_SQRT2, comb=comb, comb_w=comb_w, comb_b=comb_b)
-        assert x1 is None
-        return ops.conv2d(a1, e["w1"], 3, m.cout, bias=e["b1"], res=x0, out_scale=INV_SQRT2,
+        assert t1 is None
+        return self._conv(a1, e["w1"], 3, m.cout, bias=e["b1"], res=t0, out_scale=INV_SQRT2,
                           comb=comb, comb_w=comb_w, comb_b=comb_b)
 
     def _attn(self, m, x):
         e = self.mw[m.idx]
-        s = ops.gn_stats(x)
-        a = ops.gn_apply(x, None, s, e["gn_g"], e["gn_b"], act=False)
-        qkv = ops.conv2d(a, e["wqkv"], 1, 3 * m.cout, bias=e["bqkv"])
+        t, s = x
+        a = ops.gn_apply(t, None, s, e["gn_g"], e["gn_b"], act=False)
+        qkv, _ = self._conv(a, e["wqkv"], 1, 3 * m.cout, bias=e["bqkv"], want_stats=False)
         o = ops.attention(qkv, m.cout)
-        return ops.conv2d(o, e["w3"], 1, m.cout, bias=e["b3"], res=x, out_scale=INV_SQRT2)
+        return self._conv(o, e["w3"], 1, m.cout, bias=e["b3"], res=t, out_scale=INV_SQRT2)
 
     def _pyramid_head(self, gn_m, conv_m, h, pyr_up):
         g = self.mw[gn_m.idx]
         c = self.mw[conv_m.idx]
-        s = ops.gn_stats(h)
-        a = ops.gn_apply(h, None, s, g["g"], g["b"], act=True)
+        a = ops.gn_apply(h[0], None, h[1], g["g"], g["b"], act=True)
         return ops.conv2d(a, c["w"], 3, 4, bias=c["b"], res=pyr_up, out_f32=True)
 
     # ------------------------------------------------------------------ forward
@@ -204,7 +212,7 @@ class NCSNppHIP:
         W = self.W
         dense = self.temb(t)
         col, pyr_in = ops.input_pack(x, y, self.dtype)
-        h = ops.conv2d(col, W["in_w"], 1, 128, bias=W["in_b"])
+        h = self._conv(col, W["in_w"], 1, 128, bias=W["in_b"])
         hs = [h]
         plan = self.plan
         i = 4

@@ -40,9 +40,10 @@ def _dev(*ts):
 
 def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_wgt=None, temb=None,
            temb_off=0, res=None, out_scale=1.0, comb=None, comb_w=None, comb_b=None, out=None,
-           out_f32=False):
+           out_f32=False, stats=None):
     """NHWC conv (see snrse_conv2d).  src0 [B,H,W,C0]; returns out [B,H,W,cout].
-    temb: [B, R] f32 table of all Dense_0 outputs, this layer's columns start at temb_off."""
+    temb: [B, R] f32 table of all Dense_0 outputs, this layer's columns start at temb_off.
+    stats: optional [B, cout, 2] f64 tensor receiving the output's per-channel (sum, sumsq)."""
     _dev(src0, src1, wgt, sc, sc1, sc_wgt, bias, res, comb, comb_w, comb_b, temb)
     B, H, W, C0 = src0.shape
     C1 = 0 if src1 is None else src1.shape[3]
@@ -54,26 +55,41 @@ def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_w
     _lib.call("snrse_conv2d", _ptr(src0), C0, _ptr(src1), C1, B, H, W, ksize, _ptr(wgt), _ptr(sc), Csc,
               _ptr(sc1), Csc1, _ptr(sc_wgt), _ptr(bias), None if temb is None else temb.data_ptr() + 4 * temb_off,
               0 if temb is None else temb.shape[1], _ptr(res), 0 if res is None else res.shape[-1], float(out_scale), _ptr(comb),
-              _ptr(comb_w), _ptr(comb_b), out.data_ptr(), cout, out.shape[-1], code(src0.dtype),
+              _ptr(comb_w), _ptr(comb_b), out.data_ptr(), cout, out.shape[-1], _ptr(stats), code(src0.dtype),
               int(out_f32), _stream())
     return out
 
 
+def new_stats(x_or_shape, C=None):
+    """Empty [B, C, 2] f64 per-channel statistics buffer for an NHWC tensor."""
+    if C is None:
+        B, C, dev = x_or_shape.shape[0], x_or_shape.shape[-1], x_or_shape.device
+    else:
+        B, dev = x_or_shape, torch.device("cuda")
+    return torch.empty(B, C, 2, device=dev, dtype=torch.float64)
+
+
 def gn_stats(src0, src1=None):
+    """Per-channel (sum, sumsq) of each source: returns (sums0, sums1 or None)."""
     _dev(src0, src1)
     B, H, W, C0 = src0.shape
     C1 = 0 if src1 is None else src1.shape[3]
-    sums = torch.empty(B, C0 + C1, 2, device=src0.device, dtype=torch.float64)
-    _lib.call("snrse_gn_stats", _ptr(src0), C0, _ptr(src1), C1, B, H * W, sums.data_ptr(),
+    s0 = new_stats(src0)
+    s1 = None if src1 is None else new_stats(src1)
+    _lib.call("snrse_gn_stats", _ptr(src0), C0, _ptr(src1), C1, B, H * W, s0.data_ptr(), _ptr(s1),
               code(src0.dtype), _stream())
-    return sums
+    return s0, s1
 
 
 MODES = {"none": 0, "down": 1, "up": 2}
 
 
-def gn_apply(src0, src1=None, sums=None, gamma=None, beta=None, act=True, mode="none", groups=None, eps=1e-6):
-    _dev(src0, src1, sums, gamma, beta)
+def gn_apply(src0, src1=None, sums=None, gamma=None, beta=None, act=True, mode="none", groups=None, eps=1e-6,
+             sums1=None):
+    """sums: per-channel stats of src0 ([B, C0, 2]) or a (sums0, sums1) pair; None = no norm."""
+    if isinstance(sums, tuple):
+        sums, sums1 = sums
+    _dev(src0, src1, sums, sums1, gamma, beta)
     B, H, W, C0 = src0.shape
     C1 = 0 if src1 is None else src1.shape[3]
     C = C0 + C1
@@ -81,8 +97,8 @@ def gn_apply(src0, src1=None, sums=None, gamma=None, beta=None, act=True, mode="
     Ho, Wo = (H // 2, W // 2) if m == 1 else ((2 * H, 2 * W) if m == 2 else (H, W))
     out = torch.empty(B, Ho, Wo, C, device=src0.device, dtype=src0.dtype)
     g = groups if groups is not None else min(C // 4, 32)
-    _lib.call("snrse_gn_apply", _ptr(src0), C0, _ptr(src1), C1, B, H, W, _ptr(sums), _ptr(gamma), _ptr(beta),
-              g, float(eps), int(bool(act)), m, out.data_ptr(), code(src0.dtype), _stream())
+    _lib.call("snrse_gn_apply", _ptr(src0), C0, _ptr(src1), C1, B, H, W, _ptr(sums), _ptr(sums1), _ptr(gamma),
+              _ptr(beta), g, float(eps), int(bool(act)), m, out.data_ptr(), code(src0.dtype), _stream())
     return out
 
 
@@ -215,3 +231,7 @@ def upfirdn2d(inp, kernel, up=1, down=1, pad=(0, 0)):
     _lib.call("snrse_upfirdn2d", x.data_ptr(), out.data_ptr(), k.data_ptr(), N * Cc, H, W, 1, kh, kw, up, up,
               down, down, pad[0], pad[1], pad[0], pad[1], code(inp.dtype), _stream())
     return out.view(N, Cc, oh, ow)
+
+
+def set_option(name: str, value: int):
+    _lib.call("snrse_set_option", name.encode(), int(value))

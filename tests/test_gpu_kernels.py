@@ -33,9 +33,12 @@ def nchw(x):
 DT = {"f32": (torch.float32, 2e-6), "bf16": (torch.bfloat16, 1e-2)}
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2])
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
-@pytest.mark.parametrize("shape", [(2, 128, 128, 8, 16), (1, 256, 128, 4, 8), (3, 128, 256, 5, 7), (2, 384, 256, 4, 4)])
-def test_conv3x3(gpu, dt, shape):
+@pytest.mark.parametrize("shape", [(2, 128, 128, 8, 16), (1, 256, 128, 4, 8), (3, 128, 256, 5, 7), (2, 384, 256, 4, 4),
+                                   (2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (1, 256, 256, 12, 64)])
+def test_conv3x3(gpu, dt, shape, variant):
+    """variant: 0 auto (halo kernel where H%4==0, W%64==0), 1 register-staged, 2 LDS-DMA im2col."""
     from snrse import ops
     dtype, tol = DT[dt]
     B, cin, cout, H, W = shape
@@ -49,16 +52,22 @@ def test_conv3x3(gpu, dt, shape):
     xg = nhwc(x).to(gpu, dtype)
     src0, src1 = (xg[..., :c0].contiguous(), xg[..., c0:].contiguous()) if c0 != cin else (xg, None)
     wp = w.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu, dtype).contiguous()
-    out = ops.conv2d(src0, wp, 3, cout, bias=b.to(gpu), src1=src1)
+    ops.set_option("conv_variant", variant)
+    try:
+        out = ops.conv2d(src0, wp, 3, cout, bias=b.to(gpu), src1=src1)
+    finally:
+        ops.set_option("conv_variant", 0)
     assert rel(nchw(out.float()), ref) < tol
 
 
+@pytest.mark.parametrize("hw", [(8, 8), (8, 64)])
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
-def test_conv_epilogue_shortcut_temb_comb(gpu, dt):
-    """Conv_1 + Conv_2 shortcut as extra K, temb bias, residual scale and Combine term."""
+def test_conv_epilogue_shortcut_temb_comb(gpu, dt, hw):
+    """Conv_1 + Conv_2 shortcut as extra K, temb bias, residual scale, Combine term, fused stats."""
     from snrse import ops
     dtype, tol = DT[dt]
-    B, cin, cout, H, W = 2, 128, 256, 8, 8
+    B, cin, cout = 2, 128, 256
+    H, W = hw
     h = torch.from_numpy(fnormal("t.ep.h", (B, cout, H, W)))
     xs = torch.from_numpy(fnormal("t.ep.xs", (B, cin, H, W)))
     w1 = torch.from_numpy(fnormal("t.ep.w1", (cout, cout, 3, 3))) / 48
@@ -73,11 +82,16 @@ def test_conv_epilogue_shortcut_temb_comb(gpu, dt):
     ref = (F.conv2d(h.double(), w1.double(), b1.double(), padding=1) + F.conv2d(xs.double(), w2.double())
            + temb[:, 20:20 + cout, None, None].double()) / math.sqrt(2)
     ref = ref + torch.einsum("bihw,oi->bohw", pyr.double(), cw.double()) + cb.double()[None, :, None, None]
+    st = ops.new_stats(B, cout)
     out = ops.conv2d(nhwc(h).to(gpu, dtype), w1.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu, dtype).contiguous(),
                      3, cout, bias=b1.to(gpu), sc=nhwc(xs).to(gpu, dtype),
                      sc_wgt=w2.reshape(cout, cin).to(gpu, dtype).contiguous(), temb=temb.to(gpu), temb_off=20,
-                     out_scale=1 / math.sqrt(2), comb=nhwc(pyr).to(gpu), comb_w=cw.to(gpu), comb_b=cb.to(gpu))
+                     out_scale=1 / math.sqrt(2), comb=nhwc(pyr).to(gpu), comb_w=cw.to(gpu), comb_b=cb.to(gpu), stats=st)
     assert rel(nchw(out.float()), ref) < tol
+    o = out.double()
+    st_ref = torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)
+    # stats are taken from the fp32 epilogue values, the check re-sums the stored (bf16) output
+    assert rel(st, st_ref) < (1e-5 if dt == "f32" else 3e-3)
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
@@ -119,6 +133,13 @@ def test_gn_silu_fir(gpu, dt, mode, C):
     s0, s1 = (xg[..., :256].contiguous(), xg[..., 256:].contiguous()) if C == 384 else (xg, None)
     sums = ops.gn_stats(s0, s1)
     out = ops.gn_apply(s0, s1, sums, g.to(gpu), be.to(gpu), act=True, mode=mode)
+    # statistics fused into a producing GEMM's epilogue must agree with the standalone pass
+    if C == 128:
+        eye = torch.eye(C).reshape(C, C, 1, 1)
+        st = ops.new_stats(xg)
+        y2 = ops.conv2d(xg, eye.reshape(C, C).to(gpu, dtype).contiguous(), 1, C, stats=st)
+        assert torch.equal(y2, xg)
+        assert rel(st, sums[0]) < 1e-6
     assert rel(nchw(out.float()), ref) < tol
 
 

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of the conv GEMM variants on the NCSN++ shapes (interleaved A/B in one
+process, HIP events on the launch stream).  Usage: python tools/conv_bench.py [--reps 10]"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "snr-aligned_diffse_amd"))
+
+import torch  # noqa: E402
+
+from snrse import ops  # noqa: E402
+
+# (B, C0, C1, Cout, H, W, ksize, Csc) — the dominant per-NFE shapes at 4 s
+SHAPES = [
+    (32, 128, 0, 128, 256, 512, 3, 0),
+    (32, 128, 128, 128, 256, 512, 3, 0),   # up-path cat Conv_0
+    (32, 128, 0, 128, 256, 512, 3, 256),   # Conv_1 + 1x1 shortcut of a cat input
+    (32, 256, 0, 256, 128, 256, 3, 0),
+    (32, 256, 0, 256, 64, 128, 3, 0),
+    (32, 256, 256, 256, 32, 64, 3, 0),
+    (32, 256, 0, 768, 16, 32, 1, 0),
+]
+
+
+def run(shape, variant, reps, dev):
+    B, C0, C1, Co, H, W, k, Csc = shape
+    g = torch.Generator(device=dev).manual_seed(0)
+    x0 = torch.randn(B, H, W, C0, device=dev, generator=g).bfloat16()
+    x1 = torch.randn(B, H, W, C1, device=dev, generator=g).bfloat16() if C1 else None
+    sc = torch.randn(B, H, W, Csc, device=dev, generator=g).bfloat16() if Csc else None
+    w = (torch.randn(Co, k * k * (C0 + C1), device=dev, generator=g) / 30).bfloat16()
+    ws = (torch.randn(Co, Csc, device=dev, generator=g) / 16).bfloat16() if Csc else None
+    bias = torch.zeros(Co, device=dev)
+    st = ops.new_stats(B, Co)
+    ops.set_option("conv_variant", variant)
+    out = ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, stats=st)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, out=out, stats=st)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ts.sort()
+    fl = 2.0 * B * H * W * Co * (k * k * (C0 + C1) + Csc)
+    return out, ts[len(ts) // 2], fl
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--variants", default="1,2")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    res = []
+    for sh in SHAPES:
+        outs = {}
+        row = {"shape": sh}
+        for v in [int(x) for x in a.variants.split(",")]:
+            out, ms, fl = run(sh, v, a.reps, dev)
+            outs[v] = out.float()
+            row[f"v{v}_ms"] = ms
+            row[f"v{v}_tflops"] = fl / ms / 1e9
+        if len(outs) > 1:
+            ks = list(outs)
+            d = (outs[ks[0]] - outs[ks[1]]).abs().max().item()
+            row["max_abs_diff"] = d
+        res.append(row)
+        print(json.dumps(row), flush=True)
+    ops.set_option("conv_variant", 0)
+
+
+if __name__ == "__main__":
+    main()
