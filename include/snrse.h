@@ -17,6 +17,7 @@
 #ifndef SNRSE_H_
 #define SNRSE_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -125,6 +126,20 @@ int snrse_stft(const float* sig, int B, int L, const float* in_div, float in_sca
  * f32, times out_scale[b] (NULL = 1).  frames: workspace of B*T*510 floats. */
 int snrse_istft(const void* spec, int B, int T, int L, int mode, const float* out_scale, float* frames,
                 float* out, hipStream_t stream);
+
+/* Exponent spectrogram transform on interleaved complex64 (data_module.py:241-267):
+ * dir 0 = spec_fwd (|c|^0.5 e^{i angle c} * 0.15), dir 1 = spec_back (inverse).  In place allowed. */
+int snrse_spec_transform(const void* in, void* out, long long n, int dir, hipStream_t stream);
+
+/* SNR estimator SNRNet.forward (snrnet.py:47-97) on the raw complex STFT spec [B][256][T]
+ * (T % 16 == 0): out[b] = sigmoid(...) in (0, 1).  Weights f32 in torch layouts (see
+ * csrc/snrnet.hip); ws: workspace of snrse_snrnet_workspace(B, T) bytes. */
+int snrse_snrnet(const void* spec, int B, int T, const float* w5, const float* b5, const float* w3,
+                 const float* b3, const float* wt1, const float* wt2, const float* wt3, const float* wt4,
+                 const float* bt1, const float* bt2, const float* bt3, const float* bt4, const float* wih,
+                 const float* bsum, const float* whh, const float* fcw, const float* fcb, float* ws,
+                 float* out, hipStream_t stream);
+size_t snrse_snrnet_workspace(int B, int T);
 
 #ifdef __cplusplus
 }

@@ -159,7 +159,34 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* sig, int L, fl
   if (threadIdx.x == 0) out[b] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
+// spec_fwd / spec_back of the 'exponent' transform on interleaved complex64 (e = 0.5, factor 0.15)
+__global__ __launch_bounds__(256) void spec_transform_kernel(const float2* in, float2* out, long long n, int dir) {
+  const long long i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= n) return;
+  float2 v = in[i];
+  if (dir == 0) {
+    const float mag = sqrtf(v.x * v.x + v.y * v.y);
+    const float g = mag > 0.f ? 0.15f / sqrtf(mag) : 0.f;
+    v.x *= g;
+    v.y *= g;
+  } else {
+    v.x *= (1.0f / 0.15f);
+    v.y *= (1.0f / 0.15f);
+    const float mag = sqrtf(v.x * v.x + v.y * v.y);
+    v.x *= mag;
+    v.y *= mag;
+  }
+  out[i] = v;
+}
+
 }  // namespace
+
+extern "C" int snrse_spec_transform(const void* in, void* out, long long n, int dir, hipStream_t s) {
+  if (n <= 0 || !in || !out || (dir != 0 && dir != 1)) return SNRSE_EINVAL;
+  hipLaunchKernelGGL(spec_transform_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float2*)in,
+                     (float2*)out, n, dir);
+  return (int)hipGetLastError();
+}
 
 extern "C" int snrse_absmax(const float* sig, int B, int L, float* out, hipStream_t s) {
   if (B <= 0 || L <= 0 || !sig || !out) return SNRSE_EINVAL;

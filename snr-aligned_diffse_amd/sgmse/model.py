@@ -1,0 +1,272 @@
+"""ScoreModel — inference half of the reference's sgmse/model.py (ScoreModel, 32-1016).
+
+Same constructor / attribute / method surface that eval.py and deep_eval.py use
+(load_from_checkpoint, eval(no_ema), sde, dnn, enhance, forward, get_pc_sampler, to_audio,
+_stft, _istft, _forward_transform, _backward_transform, t_eps, sigma_max, fixed_snr,
+model_type, snr_conditioned) on top of the HIP runtime.  Training (_step, validation,
+optimizer hooks) and the dead debug helpers (enhance_debug, prior_tests2, get_prior) are
+out of scope.
+
+Defined behaviour where the reference cannot run:
+  * sebridge forward accepts t of shape [B] as well as [B,1,1,1] (the reference's
+    t.squeeze(3) fails on the PC sampler's [B] time vector), so PC sampling works for every
+    model_type;
+  * enhance(timeit=True) reports nfe = 1 on the one-step branches (undefined in the reference);
+  * the SNR-estimator checkpoint is loaded lazily on first use instead of at import (the
+    reference loads './sgmse-bbed/sgmse/snr_estimator.ckpt' onto CUDA when the module is
+    imported, model.py:25-30); its path can be overridden with SNRSE_SNR_CKPT.
+"""
+from __future__ import annotations
+
+import os
+import time
+import warnings
+from math import ceil
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from snrse import ops
+from snrse import sampler as _samp
+
+from . import sampling
+from .backbones import BackboneRegistry
+from .data_module import SpecsDataModule
+from .ema import EMAState, load_checkpoint
+from .sdes import SDERegistry
+from .util.other import pad_spec, pad_spec_16, snr_dB  # noqa: F401  (re-exported like the reference)
+
+i_30 = np.arange(1, 30 + 1)
+t_30 = (0.001 ** (1 / 7) + (i_30 - 1) / (30 - 1) * (1 ** (1 / 7) - 0.001 ** (1 / 7))) ** 7
+
+SNR_CKPT = os.environ.get("SNRSE_SNR_CKPT", "./sgmse-bbed/sgmse/snr_estimator.ckpt")
+_snr_model = None
+
+
+def get_snr_model():
+    """The SNR estimator used by enhance() when snr_conditioned == 'true' and oracle is off."""
+    global _snr_model
+    if _snr_model is None:
+        from .snr_estimator import SNRModel
+        if not os.path.exists(SNR_CKPT):
+            raise FileNotFoundError(f"SNR-estimator checkpoint not found at {SNR_CKPT}; set SNRSE_SNR_CKPT or "
+                                    "call enhance(..., oracle=True, clean_rms=..., noise_rms=...)")
+        m = SNRModel.load_from_checkpoint(SNR_CKPT, base_dir="", batch_size=1, num_workers=0)
+        m.eval()
+        _snr_model = m.to("cuda")
+    return _snr_model
+
+
+def set_snr_model(model):
+    global _snr_model
+    _snr_model = model
+
+
+def _noise_seed():
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
+
+
+class ScoreModel(nn.Module):
+    @staticmethod
+    def add_argparse_args(parser):
+        parser.add_argument("--lr", type=float, default=1e-4, help="The learning rate (1e-4 by default)")
+        parser.add_argument("--ema_decay", type=float, default=0.999, help="The parameter EMA decay constant")
+        parser.add_argument("--t_eps", type=float, default=0.03, help="The minimum time (3e-2 by default)")
+        parser.add_argument("--num_eval_files", type=int, default=10)
+        parser.add_argument("--loss_type", type=str, default="mse")
+        parser.add_argument("--loss_abs_exponent", type=float, default=0.5)
+        return parser
+
+    def __init__(self, backbone, sde, model_type="sebridge", snr_conditioned="false", fixed_snr=1.0, lr=1e-4,
+                 ema_decay=0.999, t_eps=3e-2, loss_abs_exponent=0.5, num_eval_files=10, loss_type="mse",
+                 data_module_cls=None, **kwargs):
+        super().__init__()
+        self.dnn = BackboneRegistry.get_by_name(backbone)(**kwargs)
+        if sde == "bbve":  # old checkpoints (model.py:67-74)
+            sde = "bbed"
+            kwargs["k"] = kwargs.pop("sigma_max")
+            kwargs.pop("sigma_min", None)
+            kwargs.setdefault("sigma_max", kwargs["k"])
+        self.sde = SDERegistry.get_by_name(sde)(**kwargs)
+        self.sigma_max = kwargs.get("sigma_max", getattr(self.sde, "sigma_max", None))
+        self.model_type = model_type
+        self.snr_conditioned = snr_conditioned
+        self.fixed_snr = fixed_snr
+        self.lr, self.ema_decay = lr, ema_decay
+        self.ema = EMAState(self, ema_decay)
+        self.t_eps = t_eps
+        self.loss_type, self.num_eval_files, self.loss_abs_exponent = loss_type, num_eval_files, loss_abs_exponent
+        self.hparams = dict(backbone=backbone, sde=sde, model_type=model_type, snr_conditioned=snr_conditioned,
+                            fixed_snr=fixed_snr, t_eps=t_eps, **kwargs)
+        dm = data_module_cls or SpecsDataModule
+        self.data_module = dm(**{k: v for k, v in kwargs.items() if k != "fixed_snr"}, fixed_snr=self.fixed_snr,
+                              gpu=kwargs.get("gpus", 0) > 0)
+
+    # ------------------------------------------------------------------ checkpoints / EMA
+    @classmethod
+    def load_from_checkpoint(cls, checkpoint_path, map_location="cpu", weights_only=None, **overrides):
+        return load_checkpoint(cls, checkpoint_path, map_location, weights_only, overrides)
+
+    def train(self, mode=True, no_ema=False):
+        res = super().train(mode)
+        self.ema.on_train(mode, no_ema)
+        return res
+
+    def eval(self, no_ema=False):
+        return self.train(False, no_ema=no_ema)
+
+    # ------------------------------------------------------------------ score
+    def _score_mode(self):
+        if self.snr_conditioned == "false" and self.model_type == "bbed":
+            return 0
+        if self.model_type in ("sebridge", "sebridge_v2", "sebridge_v3"):
+            if self.snr_conditioned == "fixed" and self.model_type == "sebridge_v2":
+                raise NotImplementedError("snr_conditioned='fixed' sebridge_v2 preconditioning (model.py:515-521)")
+            return 1
+        raise NotImplementedError(f"model_type={self.model_type!r} / snr_conditioned={self.snr_conditioned!r}")
+
+    def forward(self, x, t, y, s=None):
+        """Preconditioned score (model.py:481-543): -dnn for 'bbed', c_skip x + c_out dnn for sebridge*."""
+        if s is not None:
+            raise NotImplementedError("the sigma-conditioned forward needs NCSNpp_snr, which the reference "
+                                      "cannot call either (model.py:541 vs ncsnpp_snr.py:264)")
+        mode = self._score_mode()
+        B = x.shape[0]
+        tv = t.reshape(B, -1)[:, 0].to(torch.float32).contiguous()
+        net = self.dnn.hip(x.device)
+        xc = x.to(torch.complex64).reshape(B, x.shape[-2], x.shape[-1]).contiguous()
+        yc = y.to(torch.complex64).reshape(B, y.shape[-2], y.shape[-1]).contiguous()
+        return net.score(xc, yc, tv, mode)[:, None]
+
+    def fused_score_step(self, Yc):
+        """Step function for the PC loop: NCSN++ pyramid + output head + SDE update in one kernel."""
+        net = self.dnn.hip(Yc.device)
+        mode = self._score_mode()
+
+        def step(x, tv, coef, z, seed, off):
+            pyr = net.pyramid(x, Yc, tv)
+            xo, xm, _ = ops.score_update(pyr, net.W["out_w"], net.W["out_b"], tv, mode, x, Yc, coef=coef, noise=z,
+                                         seed=seed, offset=off)
+            return xo, xm
+
+        return step
+
+    # ------------------------------------------------------------------ samplers
+    def get_pc_sampler(self, predictor_name, corrector_name, y, Y_prior=None, N=None, minibatch=None,
+                       timestep_type=None, **kwargs):
+        N = self.sde.N if N is None else N
+        sde = self.sde.copy()
+        sde.N = N
+        kwargs = {"eps": self.t_eps, **kwargs}
+        if minibatch is None:
+            return sampling.get_pc_sampler(predictor_name, corrector_name, sde=sde, score_fn=self, Y=y,
+                                           Y_prior=Y_prior, timestep_type=timestep_type, **kwargs)
+        M = y.shape[0]
+
+        def batched_sampling_fn():
+            samples, ns = [], []
+            for i in range(int(ceil(M / minibatch))):
+                y_mini = y[i * minibatch:(i + 1) * minibatch]
+                yp = None if Y_prior is None else Y_prior[i * minibatch:(i + 1) * minibatch]
+                sampler = sampling.get_pc_sampler(predictor_name, corrector_name, sde=sde, score_fn=self, Y=y_mini,
+                                                  Y_prior=yp, **kwargs)
+                sample, n = sampler()
+                samples.append(sample)
+                ns.append(n)
+            return torch.cat(samples, dim=0), ns
+
+        return batched_sampling_fn
+
+    def get_ode_sampler(self, y, Y_prior=None, N=None, minibatch=None, timestep_type=None, **kwargs):
+        return sampling.get_ode_sampler(self.sde, self, y)
+
+    # ------------------------------------------------------------------ spectrogram glue
+    def to_audio(self, spec, length=None):
+        return self._istft(self._backward_transform(spec), length)
+
+    def _forward_transform(self, spec):
+        return self.data_module.spec_fwd(spec)
+
+    def _backward_transform(self, spec):
+        return self.data_module.spec_back(spec)
+
+    def _stft(self, sig):
+        return self.data_module.stft(sig)
+
+    def _istft(self, spec, length=None):
+        return self.data_module.istft(spec, length)
+
+    def calculate_snr_direct(self, s, n, fixed_snr):
+        return (n / s) / (10 ** 0.25 * fixed_snr)
+
+    def calculate_normfac_direct(self, s, n, fixed_snr):
+        return 2.040166 * (0.240253 + 0.759747 * fixed_snr ** 2) ** 0.5 / ((1 + (n / s) ** 2) ** 0.5)
+
+    # ------------------------------------------------------------------ enhance
+    @torch.no_grad()
+    def enhance(self, x, y, sampler_type="pc", predictor="reverse_diffusion", corrector="ald", N=30,
+                corrector_steps=1, snr=0.5, timeit=False, oracle=False, clean_rms=1, noise_rms=1, **kwargs):
+        """One-call enhancement of noisy speech y [1, L] (model.py:702-839) -> numpy [L]."""
+        start = time.time()
+        dev = torch.device("cuda", torch.cuda.current_device())
+        T_orig = y.size(1)
+        yd = y.to(dev, torch.float32).reshape(1, -1).contiguous()
+        nf = ops.absmax(yd)  # norm_factor = max|y| (model.py:726)
+        Tp = T_orig // 128 + 1
+        Tp = Tp + (64 - Tp % 64) % 64
+        noise_tape = kwargs.get("noise_tape")
+        nfe = 1
+        if self.snr_conditioned == "true":
+            if self.model_type != "sebridge_v3":
+                raise NotImplementedError("snr_conditioned='true' is implemented for model_type='sebridge_v3' "
+                                          "(the sebridge_v2 branch needs the 3-argument NCSNpp_snr)")
+            if oracle:
+                est_snr = float(noise_rms) / float(clean_rms)  # model.py:722-724
+            else:
+                T16 = T_orig // 128 + 1
+                T16 = T16 + (16 - T16 % 16) % 16
+                raw = ops.stft(yd, 1.0, tpad=T16, mode=0, in_div=nf)  # y / max|y|, raw STFT, pad_spec_16
+                est_snr = float(get_snr_model().estimate_from_spec(raw)[0])
+            t_hat = float(t_30[np.abs(t_30 - est_snr / (10 ** 0.25 * self.fixed_snr)).argmin()])
+            normfac = self.calculate_normfac_direct(1.0, 10 ** 0.25 * self.fixed_snr * t_hat, self.fixed_snr)
+            div = nf * float(normfac)
+            Y = ops.stft(yd, 1.0, tpad=Tp, mode=1, in_div=div)
+            z_scale = float(self.sigma_max) * t_hat
+            Z = noise_tape(0) if noise_tape is not None else None
+            coef = torch.tensor([[0.0, 1.0, 0.0, z_scale]], device=dev)
+            X_T = ops.axpby_noise(coef, y=Y, noise=Z, seed=_noise_seed())
+            sample = self(X_T[:, None], torch.full((1, 1, 1, 1), t_hat, device=dev), Y[:, None])[:, 0]
+            out_scale = div
+        else:
+            div = nf
+            Y = ops.stft(yd, 1.0, tpad=Tp, mode=1, in_div=div)
+            if self.model_type == "bbed":
+                if sampler_type == "pc":
+                    sampler = self.get_pc_sampler(predictor, corrector, Y[:, None], N=N, corrector_steps=corrector_steps,
+                                                  snr=snr, noise_tape=noise_tape)
+                elif sampler_type == "ode":
+                    sampler = self.get_ode_sampler(Y[:, None], N=N, **kwargs)
+                else:
+                    raise ValueError(f"{sampler_type} is not a valid sampler type!")
+                sample, nfe = sampler()
+                sample = sample[:, 0]
+            elif self.model_type in ("sebridge", "sebridge_v2"):
+                t = 0.999
+                zs = 0.0 if self.model_type == "sebridge" else float(self.sigma_max) * t
+                Z = noise_tape(0) if (noise_tape is not None and zs) else None
+                X_T = ops.axpby_noise(torch.tensor([[0.0, 1.0, 0.0, zs]], device=dev), y=Y, noise=Z,
+                                      seed=_noise_seed())
+                sample = self(X_T[:, None], torch.full((1, 1, 1, 1), t, device=dev), Y[:, None])[:, 0]
+            else:
+                raise NotImplementedError(f"model_type={self.model_type!r} with snr_conditioned='false'")
+            out_scale = div
+        x_hat = ops.istft(sample.contiguous(), T_orig, mode=1, out_scale=out_scale.reshape(1).contiguous())
+        x_hat = x_hat[0].cpu().numpy()
+        if timeit:
+            rtf = (time.time() - start) / (len(x_hat) / 16000)
+            return x_hat, nfe, rtf
+        return x_hat
+
+
+__all__ = ["ScoreModel", "t_30", "get_snr_model", "set_snr_model", "warnings"]

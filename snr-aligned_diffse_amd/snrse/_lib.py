@@ -37,10 +37,12 @@ SIGNATURES = {
     "snrse_axpby_noise": [_vp, _vp, _vp, _u64, _u64, _vp, _i, _i, _vp, _vp],
     "snrse_stft": [_vp, _i, _i, _vp, _f, _i, _i, _vp, _vp],
     "snrse_absmax": [_vp, _i, _i, _vp, _vp],
+    "snrse_spec_transform": [_vp, _vp, C.c_longlong, _i, _vp],
+    "snrse_snrnet": [_vp, _i, _i] + [_vp] * 17 + [_vp, _vp, _vp],
     "snrse_istft": [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
 }
 HOUSEKEEPING = {"snrse_abi_version": ([], _i), "snrse_error_string": ([_i], C.c_char_p),
-                "snrse_device_name": ([C.c_char_p, _i], _i)}
+                "snrse_device_name": ([C.c_char_p, _i], _i), "snrse_snrnet_workspace": ([_i, _i], C.c_size_t)}
 
 _lib = None
 
@@ -79,4 +81,7 @@ def check(rc: int, what: str):
 
 def call(name: str, *args):
     lib = load()
+    n = len(SIGNATURES[name])
+    if len(args) != n:  # ctypes would silently pass surplus arguments as C ints
+        raise TypeError(f"{name} takes {n} arguments, {len(args)} given")
     check(getattr(lib, name)(*args), name)

@@ -235,3 +235,37 @@ def upfirdn2d(inp, kernel, up=1, down=1, pad=(0, 0)):
 
 def set_option(name: str, value: int):
     _lib.call("snrse_set_option", name.encode(), int(value))
+
+
+def spec_transform(spec, direction):
+    """'exponent' spec_fwd (direction 0) / spec_back (1) on a complex64 device tensor."""
+    _dev(spec)
+    out = torch.empty_like(spec)
+    _lib.call("snrse_spec_transform", spec.data_ptr(), out.data_ptr(), spec.numel(), int(direction), _stream())
+    return out
+
+
+SNRNET_KEYS = ["conv5x5_1.weight", "conv5x5_1.bias", "conv3x3_1.weight", "conv3x3_1.bias", "convt_1.weight",
+               "convt_2.weight", "convt_3.weight", "convt_4.weight", "convt_1.bias", "convt_2.bias", "convt_3.bias",
+               "convt_4.bias"]
+
+
+def pack_snrnet(sd, device):
+    f = lambda k: sd[k].detach().to(device, torch.float32).contiguous()  # noqa: E731
+    w = [f(k) for k in SNRNET_KEYS]
+    wih = torch.stack([f("blstm.weight_ih_l0"), f("blstm.weight_ih_l0_reverse")]).contiguous()
+    whh = torch.stack([f("blstm.weight_hh_l0"), f("blstm.weight_hh_l0_reverse")]).contiguous()
+    bsum = torch.stack([f("blstm.bias_ih_l0") + f("blstm.bias_hh_l0"),
+                        f("blstm.bias_ih_l0_reverse") + f("blstm.bias_hh_l0_reverse")]).contiguous()
+    return w + [wih, bsum, whh, f("fc.weight").reshape(-1).contiguous(), f("fc.bias")]
+
+
+def snrnet(spec, packed):
+    """SNRNet on the raw complex STFT [B, 256, T] (T % 16 == 0) -> [B] in (0, 1)."""
+    _dev(spec)
+    B, _, T = spec.shape
+    ws = torch.empty(int(_lib.load().snrse_snrnet_workspace(B, T)) // 4 + 1, device=spec.device, dtype=torch.float32)
+    out = torch.empty(B, device=spec.device, dtype=torch.float32)
+    _lib.call("snrse_snrnet", spec.data_ptr(), B, T, *[p.data_ptr() for p in packed], ws.data_ptr(), out.data_ptr(),
+              _stream())
+    return out

@@ -73,7 +73,7 @@ def timesteps(T, N, eps):
     return torch.linspace(T, eps, N, dtype=torch.float32).double().numpy()
 
 
-def build_schedule(sde: SDESpec, N, eps, predictor, corrector, snr, corrector_steps):
+def build_schedule(sde: SDESpec, N, eps, predictor, corrector, snr, corrector_steps, probability_flow=False):
     """List of ('corr'|'pred', t, (a, by, c, s)) in execution order + prior coefficient."""
     ts = timesteps(sde.T, N, eps)
     steps = []
@@ -90,13 +90,16 @@ def build_schedule(sde: SDESpec, N, eps, predictor, corrector, snr, corrector_st
         elif corrector != "none":
             raise ValueError(f"Corrector with name '{corrector}' unknown.")
         kap = sde.drift_coef(t)
+        pf = 0.5 if probability_flow else 1.0
         if predictor == "reverse_diffusion":
             G = sde.g(t) * math.sqrt(stepsize)
-            steps.append(("pred", t, (1.0 + kap * stepsize, -kap * stepsize, G * G, G)))
+            steps.append(("pred", t, (1.0 + kap * stepsize, -kap * stepsize, pf * G * G,
+                                      0.0 if probability_flow else G)))
         elif predictor == "euler_maruyama":
             dt = -1.0 / N
             g = sde.g(t)
-            steps.append(("pred", t, (1.0 - kap * dt, kap * dt, -g * g * dt, g * math.sqrt(-dt))))
+            steps.append(("pred", t, (1.0 - kap * dt, kap * dt, -pf * g * g * dt,
+                                      0.0 if probability_flow else g * math.sqrt(-dt))))
         elif predictor == "none":
             steps.append(("none", t, None))
         else:
@@ -122,13 +125,13 @@ class NoiseSource:
 
 def pc_sample(score_step, Y, sde: SDESpec, N=30, eps=0.03, snr=0.5, predictor="reverse_diffusion",
               corrector="ald", corrector_steps=1, noise: NoiseSource | None = None, denoise=True,
-              score_tensor=None):
+              score_tensor=None, Y_prior=None, probability_flow=False):
     """Run the PC loop.  Y: complex64 [B, F, T] (device).
     score_step(x, t_vec, coef_row, z, seed, offset) -> (x_new, x_mean) runs the network + fused step;
     score_tensor(x, t_vec) -> complex score (only needed for the Langevin corrector).
     Returns (x_result, nfe)."""
     noise = noise or NoiseSource()
-    steps, prior, ns = build_schedule(sde, N, eps, predictor, corrector, snr, corrector_steps)
+    steps, prior, ns = build_schedule(sde, N, eps, predictor, corrector, snr, corrector_steps, probability_flow)
     B = Y.shape[0]
     dev = Y.device
     numel = Y.numel()
@@ -137,7 +140,7 @@ def pc_sample(score_step, Y, sde: SDESpec, N=30, eps=0.03, snr=0.5, predictor="r
     ttab = torch.tensor(np.repeat(np.asarray([t for _, t, _ in steps], dtype=np.float32)[:, None], B, axis=1),
                         device=dev)
     z, off = noise.next(numel)
-    x = ops.axpby_noise(ctab[-1], y=Y, noise=z, seed=noise.seed, offset=off)
+    x = ops.axpby_noise(ctab[-1], y=Y if Y_prior is None else Y_prior, noise=z, seed=noise.seed, offset=off)
     x_mean = x
     ci = 0
     for si, (kind, t, cf) in enumerate(steps):

@@ -1,0 +1,101 @@
+"""GPU parity of the drop-in sgmse API (through the C-ABI) against the reference goldens."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import fnormal, formula_sd, golden
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).detach().cpu()
+    b = torch.as_tensor(b).detach().cpu()
+    dt = torch.complex128 if (a.is_complex() or b.is_complex()) else torch.float64
+    a, b = a.to(dt), b.to(dt)
+    return float((a - b).abs().pow(2).mean().sqrt() / (b.abs().pow(2).mean().sqrt() + 1e-30))
+
+
+def score_model(model_type="bbed", snr_conditioned="false", dtype="fp32", **kw):
+    from sgmse.model import ScoreModel
+    hp = dict(backbone="ncsnpp", sde="ouve", model_type=model_type, snr_conditioned=snr_conditioned, theta=1.5,
+              sigma_min=0.05, sigma_max=0.5, N=30, compute_dtype=dtype)
+    hp.update(kw)
+    m = ScoreModel(**hp)
+    sd = {k: torch.from_numpy(v) for k, v in formula_sd("ncsnpp").items()}
+    m.dnn.load_state_dict(sd)
+    return m.cuda().eval()
+
+
+def test_pc_sampler_golden(gpu):
+    g = golden("pc_ouve.npz")
+    m = score_model()
+    Y = (torch.from_numpy(fnormal("golden.pc.Y", (2, 1, 256, 64), complex_=True)) * 0.5).to(gpu)
+
+    def tape(i):
+        return torch.from_numpy(fnormal(f"golden.pc.noise.{i}", (2, 1, 256, 64), complex_=True)).to(gpu).reshape(2, 256, 64)
+
+    sampler = m.get_pc_sampler("reverse_diffusion", "ald", Y, N=5, snr=0.5, noise_tape=tape)
+    x, ns = sampler()
+    assert ns == 10 and x.shape == Y.shape
+    assert rel(x, g["out"]) < 1e-4
+
+
+def test_forward_preconditioning(gpu):
+    """ScoreModel.forward for bbed (-dnn) and sebridge_v3 (c_skip x + c_out dnn) vs the golden dnn."""
+    g = golden("ncsnpp_full.npz")
+    x = (torch.from_numpy(fnormal("golden.ncsnpp.x", (2, 2, 256, 64), complex_=True)) * 0.5).to(gpu)
+    t = torch.tensor([0.5, 0.8], device=gpu)
+    dnn = torch.from_numpy(g["out"])
+    m = score_model()
+    s = m(x[:, :1], t, x[:, 1:])
+    assert rel(s, -dnn) < 1e-4
+    m3 = score_model("sebridge_v3", "true")
+    s3 = m3(x[:, :1], t[:, None, None, None], x[:, 1:])
+    tt = t.cpu()[:, None, None, None].double()
+    c_skip = 0.25 / ((tt - 0.001) ** 2 + 0.25)
+    c_out = 0.5 * (tt - 0.001) / (0.25 + tt ** 2).sqrt()
+    ref = c_skip * x[:, :1].cpu() + c_out * dnn
+    assert rel(s3, ref) < 1e-4
+
+
+def test_enhance_sebridge_v3_oracle_golden(gpu):
+    """enhance(): one-step SNR-aligned branch (model.py:713-740, 810-833) with oracle SNR."""
+    g = golden("enhance_sebridge.npz")
+    m = score_model("sebridge_v3", "true", fixed_snr=0.17783)
+    T = 27861 // 128 + 1
+    Tp = T + (64 - T % 64) % 64
+
+    def tape(i):
+        return torch.from_numpy(fnormal("golden.enh.Z", (1, 1, 256, Tp), complex_=True)).to(gpu).reshape(1, 256, Tp)
+
+    yv = torch.from_numpy(golden("enhance_inputs.npz")["noisy_valid_i16"].astype(np.float32) / 32768.0)[None]
+    x_hat = m.enhance(yv, yv, oracle=True, clean_rms=0.09034279194278529, noise_rms=0.01521404836098084,
+                      noise_tape=tape)
+    err = rel(torch.from_numpy(x_hat), torch.from_numpy(g["x_hat"]))
+    assert err < 1e-4, err
+
+
+def test_snrnet_golden(gpu):
+    from sgmse.backbones import SNRNet
+    g = golden("snrnet.npz")
+    net = SNRNet()
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in formula_sd("snrnet", "snrnet.").items()})
+    net = net.cuda()
+    x = torch.from_numpy(fnormal("golden.snrnet.x", (2, 2, 256, 64))).to(gpu)
+    y = net(x)
+    np.testing.assert_allclose(y.cpu().numpy(), g["out"], rtol=2e-5, atol=1e-6)
+
+
+def test_data_module_golden(gpu):
+    from sgmse.data_module import SpecsDataModule
+    g = golden("stft.npz")
+    dm = SpecsDataModule()
+    y = torch.from_numpy(g["noisy_i16"].astype(np.float32) / 32768.0)
+    y = (y / y.abs().max()).to(gpu)
+    S = dm.stft(y)
+    assert rel(S, g["stft"][0]) < 1e-5
+    Sf = dm.spec_fwd(S)
+    assert rel(Sf, g["spec_fwd"][0]) < 2e-5
+    back = dm.istft(dm.spec_back(Sf), y.shape[0])
+    np.testing.assert_allclose(back.cpu().numpy(), g["roundtrip"][0], atol=2e-5)

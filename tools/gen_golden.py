@@ -330,6 +330,7 @@ def gen_sebridge_enhance():
         x_hat = istft_ref(spec_back_ref(sample.squeeze()), T_orig) * norm_factor
     save("enhance_sebridge.npz", x_hat=t2n(x_hat).reshape(-1), t_hat=np.float64(t_),
          norm_factor=t2n(norm_factor).reshape(-1), score=t2n(sample))
+    save("enhance_inputs.npz", noisy_valid_i16=noisy)
 
 
 if __name__ == "__main__":
