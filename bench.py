@@ -140,15 +140,11 @@ def main():
     ap.add_argument("--no-probe", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    from snrse import dist as sdist
+    rank, world, dev = sdist.init_from_env()
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
 
     from snrse import ncsnpp, ops, sampler
     from snrse.enhance import PCEnhancer
@@ -173,14 +169,10 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
-        chk = torch.tensor([float(xh.abs().mean())], device=dev)
-        allc = [torch.zeros_like(chk) for _ in range(world)]
-        dist.all_gather(allc, chk)  # the one metric gather over RCCL
+    elapsed = sdist.max_over_ranks(time.perf_counter() - t0, dev)
+    # per-utterance output RMS of the last step, gathered over RCCL (the one metric gather)
+    rms = xh.pow(2).mean(dim=1).sqrt().double().cpu().tolist()
+    allm = sdist.gather_metrics(rms, B * world, rank, world, dev)
     value = args.steps * B * world / elapsed
 
     roof = None
@@ -213,6 +205,7 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": 512,
                        "parallelism": f"dp{world} (utterance sharding)"},
             "roofline": roof, "cpu_baseline": cpu,
+            "output_rms_mean": float(allm.mean()),
         }
         print(json.dumps(line), flush=True)
     if dist:

@@ -1,0 +1,56 @@
+"""world_size-2 gloo run of the utterance-sharding path (CPU): shards cover every utterance
+exactly once, the max-over-ranks time and the metric gather are what rank 0 reports."""
+import os
+import socket
+
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n_total, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from snrse import dist as sd
+    r, w, dev = sd.init_from_env("gloo")
+    a, b = sd.shard_range(n_total, r, w)
+    metrics = [[float(i), float(i) * 0.5] for i in range(a, b)]  # stand-in per-utterance metrics
+    t = sd.max_over_ranks(1.0 + r, dev)
+    allm = sd.gather_metrics(metrics, n_total, r, w, dev)
+    q.put((r, a, b, t, allm.numpy().tolist()))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_sharding_ranges():
+    from snrse.dist import shard_range
+    for n in (1, 7, 32, 256, 257):
+        for w in (1, 2, 3, 8):
+            covered = []
+            for r in range(w):
+                a, b = shard_range(n, r, w)
+                covered += list(range(a, b))
+            assert covered == list(range(n))
+
+
+def test_gloo_world2_gather():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    n_total = 7
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, a0, b0, t0, m0), (r1, a1, b1, t1, m1) = res
+    assert (a0, b0, a1, b1) == (0, 4, 4, 7)
+    assert t0 == t1 == 2.0
+    assert m0 == m1 == [[float(i), float(i) * 0.5] for i in range(n_total)]
