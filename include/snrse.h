@@ -52,18 +52,28 @@ int snrse_upfirdn2d(const void* in, void* out, const float* kernel, int major, i
  *               + (comb_src ? comb_src[m][0:4] . comb_w[n][0:4] + comb_b[n] : 0)
  *   out_f32: write float output (bf16 mode pyramid heads); res then is float too.
  *   stats (optional): per-channel (sum, sumsq) of out, [B][Cout][2] double, for the next
- *          GroupNorm (zeroed by the call). */
+ *          GroupNorm (zeroed by the call).
+ *   gn_scale/gn_shift (optional, [B][C0+C1] f32, from snrse_gn_scale_shift): the main input
+ *          is consumed as SiLU(x*scale+shift) (gn_act=1) or x*scale+shift (gn_act=0), i.e. the
+ *          ResBlock's GroupNorm+SiLU fused into the GEMM's halo load (bf16, 3x3, H%4==0,
+ *          W%64==0 only; otherwise hipErrorInvalidValue). */
 int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, int B, int H, int W, int ksize,
                  const void* wgt, const void* sc_src, int Csc, const void* sc_src1, int Csc1,
                  const void* sc_wgt, const float* bias, const float* temb, int temb_stride,
                  const void* res, int res_ld, float out_scale, const float* comb_src,
                  const float* comb_w, const float* comb_b, void* out, int Cout, int out_ld,
-                 double* stats, int dtype, int out_f32, hipStream_t stream);
+                 double* stats, const float* gn_scale, const float* gn_shift, int gn_act, int dtype,
+                 int out_f32, hipStream_t stream);
 
 /* GroupNorm statistics (nn.GroupNorm, layerspp.py:221,233): per-channel (sum, sumsq) over
  * H*W of src0 into sums [B][C0][2] and of src1 into sums1 [B][C1][2] (double; zeroed by the call). */
 int snrse_gn_stats(const void* src0, int C0, const void* src1, int C1, int B, int HW, double* sums,
                    double* sums1, int dtype, hipStream_t stream);
+
+/* Per-(b, c) GroupNorm scale/shift from per-channel sums (of src0 | src1, H*W pixels each). */
+int snrse_gn_scale_shift(const double* sums0, int C0, const double* sums1, int C1, int B, int HW,
+                         const float* gamma, const float* beta, int groups, float eps, float* scale,
+                         float* shift, hipStream_t stream);
 
 /* Fused GroupNorm-apply (+SiLU) (+FIR [1,3,3,1] down/up x2) (layerspp.py:245-257,
  * up_or_down_sampling.py:195-257).  sums == NULL: identity normalisation (plain FIR of x).

@@ -54,6 +54,9 @@ struct ConvParams {
   int M;
   int ntn;        // N tiles (v2 grid)
   long long bytes0, bytes1, sc_bytes0, sc_bytes1, wbytes, sc_wbytes;  // buffer extents (v2)
+  const float* gn_scale;  // optional [B][Cin] GroupNorm scale/shift applied to the main input (halo path)
+  const float* gn_shift;
+  int gn_act;             // SiLU after the GroupNorm affine
 };
 
 template <typename T>
@@ -440,25 +443,29 @@ __global__ __launch_bounds__(512) void conv_glds_kernel(ConvParams p) {
 }
 
 // ---------------------------------------------------------------------------------------
-// v3 (bf16, 3x3, H % 4 == 0, W % 64 == 0): halo tiles.  Output tile = 4 frequency rows x 64
-// frames (256 pixels) x 128 output channels.  Per 64-channel block the (4+2) x (64+2) input
-// halo is DMA'd into LDS once and all 9 taps read their A fragments from it at shifted rows
-// (the row&7 swizzle keeps every 16-row read conflict-free), so an input element crosses
-// L2 -> LDS ~1.5x per conv instead of 9x (v2).  Weight tiles (tap, channel block) stream
-// through a 3-slot ring two steps ahead.  The 1x1 shortcut K-blocks reuse the halo path
-// with the center tap only.  LDS: 2 x 56 KiB halo + 3 x 16 KiB weights = 160 KiB.
+// v4 (bf16, 3x3, H % 4 == 0, W % 64 == 0): halo tiles with fused GroupNorm-apply + SiLU.
+// Output tile = 4 frequency rows x 64 frames (256 pixels) x 128 output channels, 8 waves of
+// 64x64.  Per 64-channel block (cb) the (4+2) x (64+2) input halo is loaded ONCE through
+// registers (prefetched one phase ahead), normalised + SiLU'd there when the conv consumes
+// SiLU(GN(x)) (ResBlock Conv_0 / Conv_1, layerspp.py:245, 266), and written to a single
+// LDS halo image that all 9 taps read at shifted rows (row&7 swizzle: conflict-free for any
+// 16-row window).  Weight tiles stream by LDS-DMA into a 2-slot ring, three taps per slot,
+// so each barrier is followed by 96 MFMAs per wave.  1x1 shortcut K-blocks (Conv_2 of the
+// same ResBlock) run as one-tap phases over the raw shortcut input.
+// LDS: 56 KiB halo + 2 x 48 KiB weights = 152 KiB (one 512-thread block per CU).
 template <typename TO>
 __global__ __launch_bounds__(512) void conv_halo_kernel(ConvParams p) {
   constexpr int TH = 4, TW = 64, HC = TW + 2;
   constexpr int HROWS = (TH + 2) * HC;       // 396
-  constexpr int HJ = 7;                      // DMA instructions per wave per halo (448 rows)
-  constexpr int HALO_BYTES = 8 * HJ * 1024;  // 57344
-  constexpr int BJ = 2, B_BYTES = 128 * 128;
+  constexpr int HJ = 7;                      // 16-B halo chunks per thread (448 rows x 8 / 512)
+  constexpr int HALO_BYTES = 448 * 128;      // 57344
+  constexpr int TAPB = 128 * 128;            // one tap's 128 x 64 bf16 weight tile
+  constexpr int SLOT = 3 * TAPB;
   constexpr int FM = 4, FN = 4, KT = 64;
   static_assert(8 * HJ * 8 >= HROWS, "halo rows");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const halo0 = smem;
-  char* const bring = smem + 2 * HALO_BYTES;
+  char* const halo = smem;
+  char* const ring = smem + HALO_BYTES;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -479,11 +486,13 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(ConvParams p) {
   const int Csc_all = p.Csc + p.Csc1;
   const int cbs = p.sc_src ? Csc_all / KT : 0;
   const int ncb = cbm + cbs;
-  const int S = 9 * cbm + cbs;
+  const int nq = 3 * cbm + cbs;
   const int K1 = 9 * Cin;
   const int slot = lane & 7;
+  const int csel = slot ^ (lane >> 3);  // source chunk of this lane (row & 7 == lane >> 3)
+  const bool gn = p.gn_scale != nullptr;
 
-  int hpix[HJ], hch[HJ];
+  int hpix[HJ];
   bool hok[HJ];
 #pragma unroll
   for (int j = 0; j < HJ; ++j) {
@@ -492,60 +501,85 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(ConvParams p) {
     const int ih = h0 + hy - 1, iw = w0 + hx - 1;
     hok[j] = hr < HROWS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
     hpix[j] = (bb * p.H + ih) * p.W + iw;
-    hch[j] = slot ^ (hr & 7);
   }
 
-  auto step_cb = [](int s_, int cbm_) { return s_ < 9 * cbm_ ? s_ / 9 : cbm_ + (s_ - 9 * cbm_); };
-  auto step_tap = [](int s_, int cbm_) { return s_ < 9 * cbm_ ? s_ % 9 : 4; };
+  u32x4 hv[HJ];
+  float gsc[8], gsh[8];
 
-#define SNRSE_HALO(CB_)                                                                               \
+  // ---- halo(c) -> registers (+ this lane's 8 GN scale/shift values)
+#define SNRSE_HALO_LOADS(BASE_, BYTES_, CS_, CC_)                                                      \
   do {                                                                                              \
-    const int c_ = (CB_);                                                                           \
-    const void* base_;                                                                              \
-    long long bytes_;                                                                               \
-    int cs_, cc_;                                                                                   \
-    if (c_ < cbm) {                                                                                 \
-      const int ch_ = c_ * KT;                                                                      \
-      const bool u1_ = ch_ >= p.C0;                                                                 \
-      base_ = u1_ ? p.src1 : p.src0;                                                                \
-      bytes_ = u1_ ? p.bytes1 : p.bytes0;                                                           \
-      cs_ = u1_ ? p.C1 : p.C0;                                                                      \
-      cc_ = u1_ ? ch_ - p.C0 : ch_;                                                                 \
-    } else {                                                                                        \
-      const int ch_ = (c_ - cbm) * KT;                                                              \
-      const bool u1_ = ch_ >= p.Csc;                                                                \
-      base_ = u1_ ? p.sc_src1 : p.sc_src;                                                           \
-      bytes_ = u1_ ? p.sc_bytes1 : p.sc_bytes0;                                                     \
-      cs_ = u1_ ? p.Csc1 : p.Csc;                                                                   \
-      cc_ = u1_ ? ch_ - p.Csc : ch_;                                                                \
-    }                                                                                               \
-    const __amdgpu_buffer_rsrc_t r_ = make_rsrc(base_, bytes_);                                     \
-    char* dst_ = halo0 + (c_ & 1) * HALO_BYTES;                                                     \
+    const __amdgpu_buffer_rsrc_t r_ = make_rsrc((BASE_), (BYTES_));                                 \
+    const int cs_ = (CS_), cc_ = (CC_) + csel * 8;                                                  \
     _Pragma("unroll") for (int j = 0; j < HJ; ++j) {                                                \
-      const unsigned voff_ = hok[j] ? (unsigned)((hpix[j] * cs_ + cc_ + hch[j] * 8) * 2) : 0x80000000u; \
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                     \
-          r_, (__attribute__((address_space(3))) void*)(dst_ + (wid * HJ + j) * 1024), 16, voff_, 0, 0, 0); \
+      const int voff_ = hok[j] ? (hpix[j] * cs_ + cc_) * 2 : (int)0x80000000;                       \
+      hv[j] = __builtin_amdgcn_raw_buffer_load_b128(r_, voff_, 0, 0);                               \
     }                                                                                               \
   } while (0)
-
-#define SNRSE_WTILE(S_)                                                                               \
-  do {                                                                                              \
-    const int s_ = (S_);                                                                            \
-    const int c_ = step_cb(s_, cbm), t_ = step_tap(s_, cbm);                                        \
-    const void* wb_;                                                                                \
-    long long wbytes_;                                                                              \
-    int wld_, koff_;                                                                                \
-    if (c_ < cbm) { wb_ = p.wgt; wbytes_ = p.wbytes; wld_ = K1; koff_ = t_ * Cin + c_ * KT; }       \
-    else { wb_ = p.sc_wgt; wbytes_ = p.sc_wbytes; wld_ = Csc_all; koff_ = (c_ - cbm) * KT; }        \
-    const __amdgpu_buffer_rsrc_t r_ = make_rsrc(wb_, wbytes_);                                      \
-    char* dst_ = bring + (s_ % 3) * B_BYTES;                                                        \
-    _Pragma("unroll") for (int j = 0; j < BJ; ++j) {                                                \
-      const int row_ = (wid * BJ + j) * 8 + (lane >> 3);                                            \
-      const unsigned voff_ = (unsigned)(((n0 + row_) * wld_ + koff_ + (slot ^ (row_ & 7)) * 8) * 2); \
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(                                                     \
-          r_, (__attribute__((address_space(3))) void*)(dst_ + (wid * BJ + j) * 1024), 16, voff_, 0, 0, 0); \
-    }                                                                                               \
-  } while (0)
+  auto halo_load = [&](int c) {
+    if (c < cbm) {
+      const int ch = c * KT;
+      if (ch < p.C0) SNRSE_HALO_LOADS(p.src0, p.bytes0, p.C0, ch);
+      else SNRSE_HALO_LOADS(p.src1, p.bytes1, p.C1, ch - p.C0);
+      if (gn) {
+        const float* sp = p.gn_scale + (size_t)bb * Cin + ch + csel * 8;
+        const float* hp = p.gn_shift + (size_t)bb * Cin + ch + csel * 8;
+        const f32x4 s0 = *(const f32x4*)sp, s1 = *(const f32x4*)(sp + 4);
+        const f32x4 t0 = *(const f32x4*)hp, t1 = *(const f32x4*)(hp + 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { gsc[i] = s0[i]; gsc[4 + i] = s1[i]; gsh[i] = t0[i]; gsh[4 + i] = t1[i]; }
+      }
+    } else {
+      const int ch = (c - cbm) * KT;
+      if (ch < p.Csc) SNRSE_HALO_LOADS(p.sc_src, p.sc_bytes0, p.Csc, ch);
+      else SNRSE_HALO_LOADS(p.sc_src1, p.sc_bytes1, p.Csc1, ch - p.Csc);
+    }
+  };
+#undef SNRSE_HALO_LOADS
+  // ---- registers -> (GN + SiLU) -> LDS halo image
+  auto halo_store = [&](int c) {
+    const bool tr = gn && c < cbm;
+#pragma unroll
+    for (int j = 0; j < HJ; ++j) {
+      u32x4 v = hv[j];
+      if (tr) {
+        if (hok[j]) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float lo = __uint_as_float(v[i] << 16), hi = __uint_as_float(v[i] & 0xffff0000u);
+            lo = fmaf(lo, gsc[2 * i], gsh[2 * i]);
+            hi = fmaf(hi, gsc[2 * i + 1], gsh[2 * i + 1]);
+            if (p.gn_act) { lo = silu(lo); hi = silu(hi); }
+            v[i] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+          }
+        } else {
+          v = u32x4{0u, 0u, 0u, 0u};
+        }
+      }
+      *(u32x4*)(halo + ((wid * HJ + j) * 8 + (lane >> 3)) * 128 + slot * 16) = v;
+    }
+  };
+  // ---- weights of phase q -> ring slot q & 1 (LDS-DMA)
+  auto wload = [&](int q) {
+    int c, t0, nt;
+    if (q < 3 * cbm) { c = q / 3; t0 = (q - c * 3) * 3; nt = 3; }
+    else { c = cbm + (q - 3 * cbm); t0 = 4; nt = 1; }
+    const bool mainw = c < cbm;
+    const int wld = mainw ? K1 : Csc_all;
+    const int kb = mainw ? c * KT : (c - cbm) * KT;
+    const __amdgpu_buffer_rsrc_t r = mainw ? make_rsrc(p.wgt, p.wbytes) : make_rsrc(p.sc_wgt, p.sc_wbytes);
+    char* dst = ring + (q & 1) * SLOT;
+    for (int jt = 0; jt < nt; ++jt) {
+      const int koff = c < cbm ? (t0 + jt) * Cin + kb : kb;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = (wid * 2 + i) * 8 + (lane >> 3);
+        const unsigned voff = (unsigned)(((n0 + row) * wld + koff + (slot ^ (row & 7)) * 8) * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            r, (__attribute__((address_space(3))) void*)(dst + jt * TAPB + (wid * 2 + i) * 1024), 16, voff, 0, 0, 0);
+      }
+    }
+  };
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -553,59 +587,51 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(ConvParams p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  SNRSE_HALO(0);
-  SNRSE_WTILE(0);
-  if (S > 1) SNRSE_WTILE(1);
+  halo_load(0);
+  wload(0);
+  halo_store(0);
   const int lrow = lane & 15, lg = lane >> 4;
-  int prev_halo_cb = -1;  // cb whose halo was issued in the previous step (-1: none)
-  int c = 0, t = 0;       // cb / tap of the current step
-  for (int s = 0; s < S; ++s) {
-    // wait: everything but the previous step's issues, unless that step issued this cb's halo
-    if (s == 0) {
-      if (S > 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (prev_halo_cb == c || s + 1 >= S) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (prev_halo_cb >= 0) {
-      asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    }
+  for (int q = 0; q < nq; ++q) {
+    int c, t0, nt;
+    if (q < 3 * cbm) { c = q / 3; t0 = (q - c * 3) * 3; nt = 3; }
+    else { c = cbm + (q - 3 * cbm); t0 = 4; nt = 1; }
+    const bool first = c < cbm ? t0 == 0 : true;
+    const bool last = c < cbm ? t0 == 6 : true;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const int ntap = c < cbm ? 9 : 1;
-    if (s + 2 < S) SNRSE_WTILE(s + 2);
-    prev_halo_cb = -1;
-    if (c + 1 < ncb && t == (ntap >= 5 ? 4 : 0)) {
-      SNRSE_HALO(c + 1);
-      prev_halo_cb = c + 1;
+    if (q + 1 < nq) wload(q + 1);
+    if (first && c + 1 < ncb) halo_load(c + 1);
+    const char* sl = ring + (q & 1) * SLOT;
+    for (int jt = 0; jt < nt; ++jt) {
+      const int tp = t0 + jt;
+      const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
+      const int hbase = (wm + dy + 1) * HC + dx + 1 + lrow;
+      const char* sb = sl + jt * TAPB;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        u32x4 af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = *(const u32x4*)(halo + swz(hbase + i * 16, 4 * k + lg));
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = *(const u32x4*)(sb + swz(wn * 64 + j * 16 + lrow, 4 * k + lg));
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<bf16_t>(af[i], bfr[j], acc[i][j]);
+      }
     }
-    const int tp = c < cbm ? t : 4;
-    const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
-    const char* ha = halo0 + (c & 1) * HALO_BYTES;
-    const char* sb = bring + (s % 3) * B_BYTES;
-    const int hbase = (wm + dy + 1) * HC + dx + 1 + lrow;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      u32x4 af[FM], bfr[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) af[i] = *(const u32x4*)(ha + swz(hbase + i * 16, 4 * k + lg));
-#pragma unroll
-      for (int j = 0; j < FN; ++j) bfr[j] = *(const u32x4*)(sb + swz(wn * 64 + j * 16 + lrow, 4 * k + lg));
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<bf16_t>(af[i], bfr[j], acc[i][j]);
+    if (last && c + 1 < ncb) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave is done reading halo(c)
+      halo_store(c + 1);
     }
-    if (++t == ntap) { t = 0; ++c; }
   }
-#undef SNRSE_HALO
-#undef SNRSE_WTILE
   epilogue<TO, FM, FN>(p, acc, (bb * p.H + h0 + wm) * p.W + w0, n0 + wn * 64, lane);
 }
 
 template <typename TO>
 int launch_halo(ConvParams p, hipStream_t s) {
-  constexpr size_t lds = 2 * 8 * 7 * 1024 + 3 * 128 * 128;
+  constexpr size_t lds = 448 * 128 + 2 * 3 * 128 * 128;
   static bool attr = false;
   if (!attr) {
     SNRSE_RET(hipFuncSetAttribute((const void*)conv_halo_kernel<TO>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -653,12 +679,15 @@ int dispatch_conv(const ConvParams& p, hipStream_t s) {
                         p.sc_bytes1 < 0x7ff00000ll;
       if (g_conv_variant != 1 && fits) {
         if (g_conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0) return launch_halo<TO>(p, s);
+        if (p.gn_scale) return SNRSE_EINVAL;  // fused GroupNorm exists only on the halo path
         if (p.Cout % 256 == 0) return launch_glds<128, 256, TO>(p, s);
         return launch_glds<256, 128, TO>(p, s);
       }
     }
+    if (p.gn_scale) return SNRSE_EINVAL;
     return launch_conv<T, TO, 128, 128, 2, 2>(p, p.Cout, s);
   }
+  if (p.gn_scale) return SNRSE_EINVAL;
   if (p.Cout > 16) return SNRSE_EINVAL;
   return launch_conv<T, TO, 128, 16, 4, 1>(p, 16, s);
 }
@@ -671,7 +700,8 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
                             const float* bias, const float* temb, int temb_stride, const void* res,
                             int res_ld, float out_scale, const float* comb_src, const float* comb_w,
                             const float* comb_b, void* out, int Cout, int out_ld, double* stats,
-                            int dtype, int out_f32, hipStream_t stream) {
+                            const float* gn_scale, const float* gn_shift, int gn_act, int dtype,
+                            int out_f32, hipStream_t stream) {
   using TrB = ConvTraits<bf16_t>;
   using TrF = ConvTraits<float>;
   const int KT = dtype == SNRSE_BF16 ? TrB::KT : TrF::KT;
@@ -689,6 +719,8 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
   p.comb_src = comb_src; p.comb_w = comb_w; p.comb_b = comb_b;
   p.out = out; p.Cout = Cout; p.out_ld = out_ld; p.M = B * H * W;
   p.stats = stats;
+  p.gn_scale = gn_scale; p.gn_shift = gn_shift; p.gn_act = gn_act;
+  if ((gn_scale == nullptr) != (gn_shift == nullptr)) return SNRSE_EINVAL;
   if (p.M <= 0) return 0;
   const long long esz = dtype == SNRSE_BF16 ? 2 : 4;
   const long long pix = (long long)B * H * W;

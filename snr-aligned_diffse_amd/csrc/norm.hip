@@ -224,7 +224,40 @@ __global__ void upfirdn2d_kernel(const T* in, T* out, const float* kern, int maj
   }
 }
 
+// scale[b][c] = gamma[c] * rstd(b, g(c)), shift[b][c] = beta[c] - mean(b, g(c)) * scale[b][c]
+__global__ __launch_bounds__(256) void gn_scale_shift_kernel(const double* sums0, int C0, const double* sums1, int C1,
+                                                             int HW, const float* gamma, const float* beta,
+                                                             int groups, float eps, float* scale, float* shift) {
+  const int b = blockIdx.x;
+  const int C = C0 + C1, cg = C / groups;
+  const double cnt = (double)cg * HW;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int g = c / cg;
+    double s = 0.0, ss = 0.0;
+    for (int k = g * cg; k < (g + 1) * cg; ++k) {
+      const double* q = k < C0 ? sums0 + ((size_t)b * C0 + k) * 2 : sums1 + ((size_t)b * C1 + k - C0) * 2;
+      s += q[0];
+      ss += q[1];
+    }
+    const double mean = s / cnt;
+    double var = ss / cnt - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float scl = (float)(1.0 / sqrt(var + (double)eps)) * gamma[c];
+    scale[(size_t)b * C + c] = scl;
+    shift[(size_t)b * C + c] = beta[c] - (float)mean * scl;
+  }
+}
+
 }  // namespace
+
+extern "C" int snrse_gn_scale_shift(const double* sums0, int C0, const double* sums1, int C1, int B, int HW,
+                                    const float* gamma, const float* beta, int groups, float eps, float* scale,
+                                    float* shift, hipStream_t stream) {
+  if (!sums0 || (C1 > 0 && !sums1) || groups <= 0 || (C0 + C1) % groups || B <= 0) return SNRSE_EINVAL;
+  hipLaunchKernelGGL(gn_scale_shift_kernel, dim3(B), dim3(256), 0, stream, sums0, C0, sums1, C1, HW, gamma, beta,
+                     groups, eps, scale, shift);
+  return (int)hipGetLastError();
+}
 
 extern "C" int snrse_gn_stats(const void* src0, int C0, const void* src1, int C1, int B, int HW,
                               double* sums, double* sums1, int dtype, hipStream_t stream) {

@@ -24,7 +24,8 @@ _vp, _i, _f, _u64 = C.c_void_p, C.c_int, C.c_float, C.c_uint64
 SIGNATURES = {
     "snrse_upfirdn2d": [_vp, _vp, _vp] + [_i] * 15 + [_vp],
     "snrse_conv2d": [_vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _i, _vp, _i, _f,
-                     _vp, _vp, _vp, _vp, _i, _i, _vp, _i, _i, _vp],
+                     _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _i, _i, _i, _vp],
+    "snrse_gn_scale_shift": [_vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _f, _vp, _vp, _vp],
     "snrse_gn_stats": [_vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _vp],
     "snrse_gn_apply": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _f, _i, _i, _vp, _i, _vp],
     "snrse_set_option": [C.c_char_p, _i],

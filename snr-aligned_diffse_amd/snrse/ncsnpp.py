@@ -168,22 +168,34 @@ class NCSNppHIP:
         return out, st
 
     def _resblock(self, m, x0, x1, dense, comb=None, comb_w=None, comb_b=None):
-        """x0/x1: (tensor, stats) of the (possibly concatenated) input."""
+        """x0/x1: (tensor, stats) of the (possibly concatenated) input.
+        Where the halo GEMM applies (bf16, 3x3, H%4 == 0, W%64 == 0) GroupNorm+SiLU is fused
+        into the GEMM's halo load; otherwise it is one gn_apply pass (with the FIR for up/down)."""
         e = self.mw[m.idx]
         mode = "up" if m.up else ("down" if m.down else "none")
         (t0, s0), (t1, s1) = x0, (x1 if x1 is not None else (None, None))
-        a0 = ops.gn_apply(t0, t1, s0, e["gn0_g"], e["gn0_b"], act=True, mode=mode, sums1=s1)
-        h, hs_ = self._conv(a0, e["w0"], 3, m.cout, bias=e["b0"], temb=dense, temb_off=e["temb_off"])
-        a1 = ops.gn_apply(h, None, hs_, e["gn1_g"], e["gn1_b"], act=True)
+        B, H, W, _ = t0.shape
+        if mode == "none" and ops.halo_ok(t0, 3, m.cout):
+            gn0 = ops.gn_scale_shift(s0, e["gn0_g"], e["gn0_b"], H * W, sums1=s1)
+            h, hs_ = self._conv(t0, e["w0"], 3, m.cout, src1=t1, gn=gn0, bias=e["b0"], temb=dense,
+                                temb_off=e["temb_off"])
+        else:
+            a0 = ops.gn_apply(t0, t1, s0, e["gn0_g"], e["gn0_b"], act=True, mode=mode, sums1=s1)
+            h, hs_ = self._conv(a0, e["w0"], 3, m.cout, bias=e["b0"], temb=dense, temb_off=e["temb_off"])
+        Hh, Wh = h.shape[1], h.shape[2]
+        if ops.halo_ok(h, 3, m.cout):
+            src, gn1 = h, ops.gn_scale_shift(hs_, e["gn1_g"], e["gn1_b"], Hh * Wh)
+        else:
+            src, gn1 = ops.gn_apply(h, None, hs_, e["gn1_g"], e["gn1_b"], act=True), None
         if "w2" in e:
             if mode != "none":
                 xs0, xs1 = ops.fir(t0, mode), None
             else:
                 xs0, xs1 = t0, t1
-            return self._conv(a1, e["w1"], 3, m.cout, bias=e["b1"], sc=xs0, sc1=xs1, sc_wgt=e["w2"],
+            return self._conv(src, e["w1"], 3, m.cout, gn=gn1, bias=e["b1"], sc=xs0, sc1=xs1, sc_wgt=e["w2"],
                               out_scale=INV_SQRT2, comb=comb, comb_w=comb_w, comb_b=comb_b)
         assert t1 is None
-        return self._conv(a1, e["w1"], 3, m.cout, bias=e["b1"], res=t0, out_scale=INV_SQRT2,
+        return self._conv(src, e["w1"], 3, m.cout, gn=gn1, bias=e["b1"], res=t0, out_scale=INV_SQRT2,
                           comb=comb, comb_w=comb_w, comb_b=comb_b)
 
     def _attn(self, m, x):

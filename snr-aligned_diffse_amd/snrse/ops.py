@@ -40,10 +40,11 @@ def _dev(*ts):
 
 def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_wgt=None, temb=None,
            temb_off=0, res=None, out_scale=1.0, comb=None, comb_w=None, comb_b=None, out=None,
-           out_f32=False, stats=None):
+           out_f32=False, stats=None, gn=None, gn_act=True):
     """NHWC conv (see snrse_conv2d).  src0 [B,H,W,C0]; returns out [B,H,W,cout].
     temb: [B, R] f32 table of all Dense_0 outputs, this layer's columns start at temb_off.
-    stats: optional [B, cout, 2] f64 tensor receiving the output's per-channel (sum, sumsq)."""
+    stats: optional [B, cout, 2] f64 tensor receiving the output's per-channel (sum, sumsq).
+    gn: optional (scale, shift) [B, C0+C1] f32 — consume SiLU(GN(x)) (halo path only, see halo_ok)."""
     _dev(src0, src1, wgt, sc, sc1, sc_wgt, bias, res, comb, comb_w, comb_b, temb)
     B, H, W, C0 = src0.shape
     C1 = 0 if src1 is None else src1.shape[3]
@@ -55,9 +56,34 @@ def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_w
     _lib.call("snrse_conv2d", _ptr(src0), C0, _ptr(src1), C1, B, H, W, ksize, _ptr(wgt), _ptr(sc), Csc,
               _ptr(sc1), Csc1, _ptr(sc_wgt), _ptr(bias), None if temb is None else temb.data_ptr() + 4 * temb_off,
               0 if temb is None else temb.shape[1], _ptr(res), 0 if res is None else res.shape[-1], float(out_scale), _ptr(comb),
-              _ptr(comb_w), _ptr(comb_b), out.data_ptr(), cout, out.shape[-1], _ptr(stats), code(src0.dtype),
-              int(out_f32), _stream())
+              _ptr(comb_w), _ptr(comb_b), out.data_ptr(), cout, out.shape[-1], _ptr(stats),
+              None if gn is None else gn[0].data_ptr(), None if gn is None else gn[1].data_ptr(), int(bool(gn_act)),
+              code(src0.dtype), int(out_f32), _stream())
     return out
+
+
+_VARIANT = {"v": 0}
+
+
+def halo_ok(x, ksize, cout):
+    """True when snrse_conv2d takes the halo path (and so accepts a fused GroupNorm)."""
+    B, H, W, C = x.shape
+    return (x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and H % 4 == 0 and W % 64 == 0
+            and _VARIANT["v"] == 0 and x.numel() * 2 < 0x7ff00000)
+
+
+def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):
+    """Per-(b, c) GroupNorm affine [B, C] x 2 from per-channel sums."""
+    _dev(sums0, sums1, gamma, beta)
+    B, C0 = sums0.shape[0], sums0.shape[1]
+    C1 = 0 if sums1 is None else sums1.shape[1]
+    C = C0 + C1
+    g = groups if groups is not None else min(C // 4, 32)
+    scale = torch.empty(B, C, device=sums0.device, dtype=torch.float32)
+    shift = torch.empty_like(scale)
+    _lib.call("snrse_gn_scale_shift", sums0.data_ptr(), C0, _ptr(sums1), C1, B, HW, gamma.data_ptr(), beta.data_ptr(),
+              g, float(eps), scale.data_ptr(), shift.data_ptr(), _stream())
+    return scale, shift
 
 
 def new_stats(x_or_shape, C=None):
@@ -235,6 +261,8 @@ def upfirdn2d(inp, kernel, up=1, down=1, pad=(0, 0)):
 
 def set_option(name: str, value: int):
     _lib.call("snrse_set_option", name.encode(), int(value))
+    if name == "conv_variant":
+        _VARIANT["v"] = int(value)
 
 
 def spec_transform(spec, direction):

@@ -312,3 +312,28 @@ def test_philox_noise_statistics(gpu):
     r = torch.view_as_real(z).double()
     assert abs(float(r.mean())) < 2e-3
     assert abs(float(r.var()) - 0.5) < 2e-3
+
+
+@pytest.mark.parametrize("shape", [(2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (2, 256, 128, 4, 64)])
+def test_conv_fused_groupnorm_silu(gpu, shape):
+    """Halo GEMM consuming SiLU(GN(x)) from raw x + per-(b,c) scale/shift (+ raw 1x1 shortcut)."""
+    from snrse import ops
+    B, cin, cout, H, W = shape
+    x = (torch.from_numpy(fnormal("t.fg.x", (B, cin, H, W))) * 1.5 + 0.2).bfloat16().float()
+    w = (torch.from_numpy(fnormal("t.fg.w", (cout, cin, 3, 3))) / math.sqrt(9 * cin)).bfloat16().float()
+    g = torch.from_numpy(fnormal("t.fg.g", (cin,))) * 0.1 + 1
+    be = torch.from_numpy(fnormal("t.fg.b", (cin,))) * 0.1
+    xs = torch.from_numpy(fnormal("t.fg.xs", (B, 128, H, W))).bfloat16().float()
+    w2 = (torch.from_numpy(fnormal("t.fg.w2", (cout, 128, 1, 1))) / 11).bfloat16().float()
+    a = F.silu(F.group_norm(x.double(), min(cin // 4, 32), g.double(), be.double(), eps=1e-6))
+    ref = F.conv2d(a, w.double(), padding=1) + F.conv2d(xs.double(), w2.double())
+    xg = nhwc(x).to(gpu, torch.bfloat16)
+    c0 = 256 if cin == 384 else cin
+    s0, s1 = (xg[..., :c0].contiguous(), xg[..., c0:].contiguous()) if c0 != cin else (xg, None)
+    sums = ops.gn_stats(s0, s1)
+    gn = ops.gn_scale_shift(sums[0], g.to(gpu), be.to(gpu), H * W, sums1=sums[1])
+    assert ops.halo_ok(s0, 3, cout)
+    out = ops.conv2d(s0, w.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu, torch.bfloat16).contiguous(), 3, cout,
+                     src1=s1, gn=gn, sc=nhwc(xs).to(gpu, torch.bfloat16),
+                     sc_wgt=w2.reshape(cout, 128).to(gpu, torch.bfloat16).contiguous())
+    assert rel(nchw(out.float()), ref) < 1e-2

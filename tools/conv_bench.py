@@ -55,10 +55,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--shapes", default="", help="comma list of SHAPES indices (default all)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     res = []
-    for sh in SHAPES:
+    sel = [SHAPES[int(i)] for i in a.shapes.split(",")] if a.shapes else SHAPES
+    for sh in sel:
         outs = {}
         row = {"shape": sh}
         for v in [int(x) for x in a.variants.split(",")]:
