@@ -51,8 +51,9 @@ int snrse_upfirdn2d(const void* in, void* out, const float* kernel, int major, i
  *   out[m][n] = ((acc + bias[n] + temb[b][n] + res[m][n]) * out_scale)
  *               + (comb_src ? comb_src[m][0:4] . comb_w[n][0:4] + comb_b[n] : 0)
  *   out_f32: write float output (bf16 mode pyramid heads); res then is float too.
- *   stats (optional): per-channel (sum, sumsq) of out, [B][Cout][2] double, for the next
- *          GroupNorm (zeroed by the call).
+ *   stats (optional): per-channel (sum, sumsq) of out, [B][SNRSE_STAT_SLOTS][Cout][2] double
+ *          (atomics spread over the slots; consumers fold them), for the next GroupNorm
+ *          (zeroed by the call).
  *   gn_scale/gn_shift (optional, [B][C0+C1] f32, from snrse_gn_scale_shift): the main input
  *          is consumed as SiLU(x*scale+shift) (gn_act=1) or x*scale+shift (gn_act=0), i.e. the
  *          ResBlock's GroupNorm+SiLU fused into the GEMM's halo load (bf16, 3x3, H%4==0,
@@ -65,8 +66,11 @@ int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, int B, int 
                  double* stats, const float* gn_scale, const float* gn_shift, int gn_act, int dtype,
                  int out_f32, hipStream_t stream);
 
+/* Statistics buffers of the GroupNorm entries: [B][SNRSE_STAT_SLOTS][C][2] double. */
+#define SNRSE_STAT_SLOTS 16
+
 /* GroupNorm statistics (nn.GroupNorm, layerspp.py:221,233): per-channel (sum, sumsq) over
- * H*W of src0 into sums [B][C0][2] and of src1 into sums1 [B][C1][2] (double; zeroed by the call). */
+ * H*W of src0 into sums and of src1 into sums1 (slotted layout above; zeroed by the call). */
 int snrse_gn_stats(const void* src0, int C0, const void* src1, int C1, int B, int HW, double* sums,
                    double* sums1, int dtype, hipStream_t stream);
 

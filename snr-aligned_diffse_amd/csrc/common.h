@@ -59,6 +59,23 @@ SNRSE_DEV double wave_sum_d(double v) {
 // dtype codes shared with the C-ABI (include/snrse.h)
 enum { SNRSE_F32 = 0, SNRSE_BF16 = 1 };
 
+// GroupNorm statistics buffers are [B][SNRSE_STAT_SLOTS][C][2] doubles: producers spread
+// their atomics over the slots (a few hundred workgroups per image would otherwise queue on
+// the same 2*C addresses), consumers sum the slots.
+#define SNRSE_STAT_SLOTS 16
+SNRSE_DEV inline size_t stat_idx(int b, int slot, int c, int C) {
+  return (((size_t)b * SNRSE_STAT_SLOTS + slot) * C + c) * 2;
+}
+// (sum, sumsq) of channel c of image b, folded over the slots
+SNRSE_DEV inline void stat_fold(const double* st, int b, int c, int C, double& s, double& ss) {
+#pragma unroll 4
+  for (int k = 0; k < SNRSE_STAT_SLOTS; ++k) {
+    const double* q = st + stat_idx(b, k, c, C);
+    s += q[0];
+    ss += q[1];
+  }
+}
+
 #define SNRSE_RET(expr)                              \
   do {                                               \
     hipError_t _e = (expr);                          \

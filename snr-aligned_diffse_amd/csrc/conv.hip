@@ -50,14 +50,33 @@ struct ConvParams {
   const float* comb_w;    // [Cout][4]
   const float* comb_b;    // [Cout]
   void* out; int Cout; int out_ld;
-  double* stats;  // optional [B][Cout][2] per-channel (sum, sumsq) of the output (zeroed by launcher)
+  double* stats;  // optional [B][SLOTS][Cout][2] per-channel (sum, sumsq) of the output (zeroed by launcher)
   int M;
   int ntn;        // N tiles (v2 grid)
   long long bytes0, bytes1, sc_bytes0, sc_bytes1, wbytes, sc_wbytes;  // buffer extents (v2)
   const float* gn_scale;  // optional [B][Cin] GroupNorm scale/shift applied to the main input (halo path)
   const float* gn_shift;
   int gn_act;             // SiLU after the GroupNorm affine
+  unsigned long long* stamps;  // timing-diagnostic build only (-DSNRSE_STAMPS): [blocks][8][32]
 };
+
+#ifdef SNRSE_STAMPS
+// Diagnostic build: s_memtime stamps of the halo kernel's segments (LDS, copied out at the
+// end).  Read their shares, never the build's run time (the stamp waits forbid overlaps).
+unsigned long long* g_stamp_buf = nullptr;
+#define SNRSE_STAMP(I)                                                                        \
+  do {                                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    unsigned long long t_;                                                                  \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    if (lane == 0) lst[(I)] = t_;                                                           \
+  } while (0)
+#else
+#define SNRSE_STAMP(I) \
+  do {                 \
+  } while (0)
+#endif
 
 template <typename T>
 SNRSE_DEV f32x4 mfma_chunk(const u32x4& a, const u32x4& b, f32x4 acc);
@@ -89,6 +108,145 @@ SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
 // Shared epilogue: y = (acc + bias + temb + res) * out_scale + combine; optional GroupNorm
 // statistics of y (per (b, channel) sum / sumsq) for the consumer's GroupNorm.
 // acc[i][j][e]: row = mb + i*16 + (lane>>4)*4 + e, col = nb + j*16 + (lane&15).
+// LDS-staged epilogue for one wave's 64 x 64 tile (rows = 64 consecutive output pixels
+// mb.., cols = output channels nb..): the fp32 accumulators go to a per-wave LDS image,
+// then every lane finishes 8 rows x one 16-byte chunk of channels, so residual loads and
+// output stores are 16-B vectors and the GN statistics need one atomic pair per channel
+// per wave.  `stage` = this wave's 64 x 68 float region (caller barriers before reuse).
+// When the whole block tile lies in one image (blk_b >= 0) the GN statistics are reduced over
+// the block's NWM wave rows in LDS (`red`, NWM x BN x 2 floats) and leave as one atomic pair per
+// channel per block; every wave of the block must call this (it holds a barrier then).
+template <typename TO, int NWM, int BN>
+SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int mb, int nb, int lane, float* stage,
+                            float* red, int wm, int blk_b, int blk_n0) {
+  constexpr int LDR = 68;  // padded row (floats): conflict-free C-layout writes
+  constexpr int EPC = 16 / (int)sizeof(TO);  // outputs per 16-B chunk (8 bf16 / 4 f32)
+  constexpr int NCH = 64 / EPC;              // chunks per row
+  constexpr int RPP = 64 / NCH;              // rows per pass of 64 lanes
+  const int lrow = lane & 15, lg = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) stage[(i * 16 + lg * 4 + e) * LDR + j * 16 + lrow] = acc[i][j][e];
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  const int HW = p.H * p.W;
+  const int cc = lane % NCH, r0 = lane / NCH;
+  const int n = nb + cc * EPC;
+  const bool nok = n < p.Cout;  // Cout % 128 == 0 on these paths; kept for safety
+  float bias[EPC], cw[EPC][4], cb[EPC];
+#pragma unroll
+  for (int k = 0; k < EPC; ++k) {
+    bias[k] = (p.bias && nok) ? p.bias[n + k] : 0.f;
+    cb[k] = 0.f;
+    cw[k][0] = cw[k][1] = cw[k][2] = cw[k][3] = 0.f;
+    if (p.comb_src && nok) {
+      cw[k][0] = p.comb_w[(n + k) * 4 + 0]; cw[k][1] = p.comb_w[(n + k) * 4 + 1];
+      cw[k][2] = p.comb_w[(n + k) * 4 + 2]; cw[k][3] = p.comb_w[(n + k) * 4 + 3];
+      cb[k] = p.comb_b[n + k];
+    }
+  }
+  const int m_last = min(mb + 63, p.M - 1);
+  const bool one_b = mb < p.M && (mb / HW) == (m_last / HW);
+  float s1[EPC], s2[EPC];
+#pragma unroll
+  for (int k = 0; k < EPC; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+#pragma unroll
+  for (int pass = 0; pass < 64 / RPP; ++pass) {
+    const int row = r0 + pass * RPP;
+    const int m = mb + row;
+    if (m >= p.M || !nok) continue;
+    float v[EPC];
+    const float* sr = stage + row * LDR + cc * EPC;
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) v[k] = sr[k] + bias[k];
+    if (p.temb) {
+      const float* tb = p.temb + (size_t)(m / HW) * p.temb_stride + n;
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) v[k] += tb[k];
+    }
+    if (p.res) {
+      const u32x4 rv = *(const u32x4*)((const TO*)p.res + (size_t)m * p.res_ld + n);
+      if constexpr (sizeof(TO) == 2) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] += __uint_as_float(rv[k] << 16);
+          v[2 * k + 1] += __uint_as_float(rv[k] & 0xffff0000u);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] += __uint_as_float(rv[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) v[k] *= p.out_scale;
+    if (p.comb_src) {
+      const f32x4 q = *(const f32x4*)(p.comb_src + (size_t)m * 4);
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) v[k] += q[0] * cw[k][0] + q[1] * cw[k][1] + q[2] * cw[k][2] + q[3] * cw[k][3] + cb[k];
+    }
+    u32x4 o;
+    if constexpr (sizeof(TO) == 2) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = (uint32_t)f2bf(v[2 * k]) | ((uint32_t)f2bf(v[2 * k + 1]) << 16);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = __float_as_uint(v[k]);
+    }
+    *(u32x4*)((TO*)p.out + (size_t)m * p.out_ld + n) = o;
+    if (p.stats) {
+      if (one_b) {
+#pragma unroll
+        for (int k = 0; k < EPC; ++k) { s1[k] += v[k]; s2[k] = fmaf(v[k], v[k], s2[k]); }
+      } else {
+#pragma unroll
+        for (int k = 0; k < EPC; ++k) {
+          const size_t o = stat_idx(m / HW, blockIdx.x & (SNRSE_STAT_SLOTS - 1), n + k, p.Cout);
+          unsafeAtomicAdd(&p.stats[o], (double)v[k]);
+          unsafeAtomicAdd(&p.stats[o + 1], (double)v[k] * v[k]);
+        }
+      }
+    }
+  }
+  if (p.stats && one_b) {
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) {
+#pragma unroll
+      for (int o = NCH; o < 64; o <<= 1) {
+        s1[k] += __shfl_xor(s1[k], o, 64);
+        s2[k] += __shfl_xor(s2[k], o, 64);
+      }
+    }
+  }
+  const int slot = blockIdx.x & (SNRSE_STAT_SLOTS - 1);
+  if (p.stats && blk_b >= 0) {  // uniform over the block
+    if (r0 == 0) {
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) {
+        red[(wm * BN + nb - blk_n0 + cc * EPC + k) * 2] = s1[k];
+        red[(wm * BN + nb - blk_n0 + cc * EPC + k) * 2 + 1] = s2[k];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int t = threadIdx.x; t < 2 * BN; t += blockDim.x) {
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWM; ++w) a += red[w * 2 * BN + t];
+      if (blk_n0 + (t >> 1) < p.Cout) unsafeAtomicAdd(&p.stats[stat_idx(blk_b, slot, blk_n0 + (t >> 1), p.Cout) + (t & 1)], (double)a);
+    }
+  } else if (p.stats && one_b && r0 == 0 && nok) {
+    const size_t base = stat_idx(mb / HW, slot, n, p.Cout);
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) {
+      unsafeAtomicAdd(&p.stats[base + 2 * k], (double)s1[k]);
+      unsafeAtomicAdd(&p.stats[base + 2 * k + 1], (double)s2[k]);
+    }
+  }
+}
+
 template <typename TO, int FM, int FN>
 SNRSE_DEV void epilogue(const ConvParams& p, const f32x4 (&acc)[FM][FN], int mb, int nb, int lane) {
   const int lrow = lane & 15, lg = lane >> 4;
@@ -127,8 +285,9 @@ SNRSE_DEV void epilogue(const ConvParams& p, const f32x4 (&acc)[FM][FN], int mb,
             s1 += v;
             s2 = fmaf(v, v, s2);
           } else {
-            unsafeAtomicAdd(&p.stats[((size_t)(m / HW) * p.Cout + n) * 2], (double)v);
-            unsafeAtomicAdd(&p.stats[((size_t)(m / HW) * p.Cout + n) * 2 + 1], (double)v * v);
+            const size_t o = stat_idx(m / HW, blockIdx.x & (SNRSE_STAT_SLOTS - 1), n, p.Cout);
+            unsafeAtomicAdd(&p.stats[o], (double)v);
+            unsafeAtomicAdd(&p.stats[o + 1], (double)v * v);
           }
         }
       }
@@ -139,7 +298,7 @@ SNRSE_DEV void epilogue(const ConvParams& p, const f32x4 (&acc)[FM][FN], int mb,
       s2 += __shfl_xor(s2, 16, 64);
       s2 += __shfl_xor(s2, 32, 64);
       if (lg == 0 && nok) {
-        const size_t o = ((size_t)(mb / HW) * p.Cout + n) * 2;
+        const size_t o = stat_idx(mb / HW, blockIdx.x & (SNRSE_STAT_SLOTS - 1), n, p.Cout);
         unsafeAtomicAdd(&p.stats[o], (double)s1);
         unsafeAtomicAdd(&p.stats[o + 1], (double)s2);
       }
@@ -439,7 +598,11 @@ __global__ __launch_bounds__(512) void conv_glds_kernel(ConvParams p) {
     stage = stage == STAGES - 1 ? 0 : stage + 1;
   }
 #undef SNRSE_ISSUE
-  epilogue<TO, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, lane);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const int b_lo = m0 / HW, b_hi = (min(m0 + BM, p.M) - 1) / HW;
+  epilogue_lds<TO, WM, BN>(p, acc, m0 + wm * TM, n0 + wn * TN, lane, (float*)(smem + wid * (64 * 68 * 4)),
+                           (float*)(smem + 8 * (64 * 68 * 4)), wm, b_lo == b_hi ? b_lo : -1, n0);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -453,7 +616,7 @@ __global__ __launch_bounds__(512) void conv_glds_kernel(ConvParams p) {
 // so each barrier is followed by 96 MFMAs per wave.  1x1 shortcut K-blocks (Conv_2 of the
 // same ResBlock) run as one-tap phases over the raw shortcut input.
 // LDS: 56 KiB halo + 2 x 48 KiB weights = 152 KiB (one 512-thread block per CU).
-template <typename TO>
+template <typename TO, bool LDS_EPI>
 __global__ __launch_bounds__(512) void conv_halo_kernel(ConvParams p) {
   constexpr int TH = 4, TW = 64, HC = TW + 2;
   constexpr int HROWS = (TH + 2) * HC;       // 396
@@ -470,6 +633,10 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(ConvParams p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
+#ifdef SNRSE_STAMPS
+  unsigned long long* const lst = (unsigned long long*)(ring + 2 * SLOT) + wid * 32;
+#endif
+  SNRSE_STAMP(0);
   const int nb = gridDim.x, bid = blockIdx.x;
   const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7, pos = bid >> 3;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
@@ -590,6 +757,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(ConvParams p) {
   halo_load(0);
   wload(0);
   halo_store(0);
+  SNRSE_STAMP(1);
   const int lrow = lane & 15, lg = lane >> 4;
   for (int q = 0; q < nq; ++q) {
     int c, t0, nt;
@@ -599,6 +767,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(ConvParams p) {
     const bool last = c < cbm ? t0 == 6 : true;
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    SNRSE_STAMP(2 + 2 * (q & 15));
     if (q + 1 < nq) wload(q + 1);
     if (first && c + 1 < ncb) halo_load(c + 1);
     const char* sl = ring + (q & 1) * SLOT;
@@ -620,27 +789,63 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(ConvParams p) {
           for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<bf16_t>(af[i], bfr[j], acc[i][j]);
       }
     }
+    SNRSE_STAMP(3 + 2 * (q & 15));
     if (last && c + 1 < ncb) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave is done reading halo(c)
       halo_store(c + 1);
     }
   }
-  epilogue<TO, FM, FN>(p, acc, (bb * p.H + h0 + wm) * p.W + w0, n0 + wn * 64, lane);
+#ifdef SNRSE_STAMPS
+  SNRSE_STAMP(28);
+  unsigned long long st_[29];
+  if (lane == 0)
+    for (int i = 0; i < 29; ++i) st_[i] = lst[i];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#endif
+  if constexpr (LDS_EPI) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // LDS is reused as the epilogue staging area
+    epilogue_lds<TO, 4, 128>(p, acc, (bb * p.H + h0 + wm) * p.W + w0, n0 + wn * 64, lane,
+                             (float*)(smem + wid * (64 * 68 * 4)), (float*)(smem + 8 * (64 * 68 * 4)), wm, bb, n0);
+  } else {
+    epilogue<TO, FM, FN>(p, acc, (bb * p.H + h0 + wm) * p.W + w0, n0 + wn * 64, lane);
+  }
+#ifdef SNRSE_STAMPS
+  {
+    unsigned long long t_end;
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_end)::"memory");
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (lane == 0 && p.stamps) {
+      unsigned long long* g = p.stamps + ((size_t)blockIdx.x * 8 + wid) * 32;
+      for (int i = 0; i < 29; ++i) g[i] = st_[i];
+      g[29] = t_end;
+      g[30] = hw;
+      g[31] = xcc;
+    }
+  }
+#endif
 }
 
-template <typename TO>
+template <typename TO, bool LDS_EPI>
 int launch_halo(ConvParams p, hipStream_t s) {
+#ifdef SNRSE_STAMPS
+  constexpr size_t lds = 448 * 128 + 2 * 3 * 128 * 128 + 8 * 32 * 8;
+#else
   constexpr size_t lds = 448 * 128 + 2 * 3 * 128 * 128;
+#endif
   static bool attr = false;
   if (!attr) {
-    SNRSE_RET(hipFuncSetAttribute((const void*)conv_halo_kernel<TO>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds));
+    SNRSE_RET(hipFuncSetAttribute((const void*)conv_halo_kernel<TO, LDS_EPI>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
   p.ntn = p.Cout / 128;
   const int tiles = p.B * (p.H / 4) * (p.W / 64);
-  hipLaunchKernelGGL((conv_halo_kernel<TO>), dim3(tiles * p.ntn), dim3(512), lds, s, p);
+  hipLaunchKernelGGL((conv_halo_kernel<TO, LDS_EPI>), dim3(tiles * p.ntn), dim3(512), lds, s, p);
   return (int)hipGetLastError();
 }
 
@@ -668,7 +873,7 @@ int launch_glds(ConvParams p, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int g_conv_variant = 0;  // 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 3 = auto
+int g_conv_variant = 0;  // 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 4 halo w/ scalar epilogue
 
 template <typename T, typename TO>
 int dispatch_conv(const ConvParams& p, hipStream_t s) {
@@ -678,7 +883,8 @@ int dispatch_conv(const ConvParams& p, hipStream_t s) {
       const bool fits = p.bytes0 < 0x7ff00000ll && p.bytes1 < 0x7ff00000ll && p.sc_bytes0 < 0x7ff00000ll &&
                         p.sc_bytes1 < 0x7ff00000ll;
       if (g_conv_variant != 1 && fits) {
-        if (g_conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0) return launch_halo<TO>(p, s);
+        if (g_conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0)
+          return g_conv_variant == 4 ? launch_halo<TO, false>(p, s) : launch_halo<TO, true>(p, s);
         if (p.gn_scale) return SNRSE_EINVAL;  // fused GroupNorm exists only on the halo path
         if (p.Cout % 256 == 0) return launch_glds<128, 256, TO>(p, s);
         return launch_glds<256, 128, TO>(p, s);
@@ -716,6 +922,11 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
   p.sc_src1 = sc_src1; p.Csc1 = sc_src ? Csc1 : 0;
   p.bias = bias; p.temb = temb; p.temb_stride = temb_stride;
   p.res = res; p.res_ld = res_ld; p.out_scale = out_scale;
+#ifdef SNRSE_STAMPS
+  p.stamps = g_stamp_buf;
+#else
+  p.stamps = nullptr;
+#endif
   p.comb_src = comb_src; p.comb_w = comb_w; p.comb_b = comb_b;
   p.out = out; p.Cout = Cout; p.out_ld = out_ld; p.M = B * H * W;
   p.stats = stats;
@@ -730,13 +941,20 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
   p.wbytes = (long long)npad * ksize * ksize * (C0 + C1) * esz;
   p.sc_wbytes = (long long)npad * (p.Csc + p.Csc1) * esz;
   p.ntn = 1;
-  if (stats) SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * (size_t)B * Cout, stream));
+  if (stats) SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * Cout, stream));
   if (dtype == SNRSE_BF16) {
     return out_f32 ? dispatch_conv<bf16_t, float>(p, stream) : dispatch_conv<bf16_t, bf16_t>(p, stream);
   }
   if (dtype == SNRSE_F32) return dispatch_conv<float, float>(p, stream);
   return SNRSE_EINVAL;
 }
+
+#ifdef SNRSE_STAMPS
+extern "C" int snrse_debug_set_stamps(void* buf) {
+  g_stamp_buf = (unsigned long long*)buf;
+  return 0;
+}
+#endif
 
 extern "C" int snrse_set_option(const char* name, int value) {
   if (!name) return SNRSE_EINVAL;

@@ -48,7 +48,7 @@ SNRSE_DEV void store_vec(T* p, const float* v) {
   *(u32x4*)p = r;
 }
 
-// grid (nblk, B), block 256.  sums0 [B][C0][2], sums1 [B][C1][2] double, zeroed by the launcher.
+// grid (nblk, B), block 256.  sums0 [B][SLOTS][C0][2], sums1 [B][SLOTS][C1][2] double, zeroed by the launcher.
 template <typename T>
 __global__ __launch_bounds__(256) void gn_stats_kernel(const T* src0, int C0, const T* src1, int C1,
                                                        int HW, int pix_per_blk, double* sums0, double* sums1) {
@@ -87,8 +87,9 @@ __global__ __launch_bounds__(256) void gn_stats_kernel(const T* src0, int C0, co
   __syncthreads();
   for (int i = tid; i < 2 * C; i += 256) {
     const int c = i >> 1;
-    if (c < C0) unsafeAtomicAdd(&sums0[((size_t)b * C0 + c) * 2 + (i & 1)], (double)red[i]);
-    else unsafeAtomicAdd(&sums1[((size_t)b * C1 + c - C0) * 2 + (i & 1)], (double)red[i]);
+    const int slot = blockIdx.x & (SNRSE_STAT_SLOTS - 1);
+    if (c < C0) unsafeAtomicAdd(&sums0[stat_idx(b, slot, c, C0) + (i & 1)], (double)red[i]);
+    else unsafeAtomicAdd(&sums1[stat_idx(b, slot, c - C0, C1) + (i & 1)], (double)red[i]);
   }
 }
 
@@ -115,9 +116,8 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const Tin* src0, int C0, 
       const int g = c / cg;
       double s = 0.0, ss = 0.0;
       for (int k = g * cg; k < (g + 1) * cg; ++k) {
-        const double* q = k < C0 ? sums + ((size_t)b * C0 + k) * 2 : sums1 + ((size_t)b * C1 + k - C0) * 2;
-        s += q[0];
-        ss += q[1];
+        if (k < C0) stat_fold(sums, b, k, C0, s, ss);
+        else stat_fold(sums1, b, k - C0, C1, s, ss);
       }
       const double mean = s / cnt;
       double var = ss / cnt - mean * mean;
@@ -235,9 +235,8 @@ __global__ __launch_bounds__(256) void gn_scale_shift_kernel(const double* sums0
     const int g = c / cg;
     double s = 0.0, ss = 0.0;
     for (int k = g * cg; k < (g + 1) * cg; ++k) {
-      const double* q = k < C0 ? sums0 + ((size_t)b * C0 + k) * 2 : sums1 + ((size_t)b * C1 + k - C0) * 2;
-      s += q[0];
-      ss += q[1];
+      if (k < C0) stat_fold(sums0, b, k, C0, s, ss);
+      else stat_fold(sums1, b, k - C0, C1, s, ss);
     }
     const double mean = s / cnt;
     double var = ss / cnt - mean * mean;
@@ -264,8 +263,8 @@ extern "C" int snrse_gn_stats(const void* src0, int C0, const void* src1, int C1
   const int V = dtype == SNRSE_BF16 ? 8 : 4;
   const int C = C0 + C1;
   if (C % V || C0 % V || C / V > 256 || !sums || (C1 > 0 && !sums1)) return SNRSE_EINVAL;
-  SNRSE_RET(hipMemsetAsync(sums, 0, sizeof(double) * 2 * C0 * B, stream));
-  if (C1 > 0) SNRSE_RET(hipMemsetAsync(sums1, 0, sizeof(double) * 2 * C1 * B, stream));
+  SNRSE_RET(hipMemsetAsync(sums, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * C0 * B, stream));
+  if (C1 > 0) SNRSE_RET(hipMemsetAsync(sums1, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * C1 * B, stream));
   int nblk = (HW + 1023) / 1024;
   if (nblk > 256) nblk = 256;
   const int ppb = (HW + nblk - 1) / nblk;

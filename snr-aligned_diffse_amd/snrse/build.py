@@ -35,18 +35,20 @@ def needs_build() -> bool:
     return any(os.path.getmtime(f) > t for f in _sources() + _headers())
 
 
-def _compile(src: str, obj: str):
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+def _compile(src: str, obj: str, extra=()):
+    cmd = [HIPCC, *FLAGS, *extra, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
     return obj
 
 
-def build_library(force: bool = False, jobs: int = 8) -> str:
-    if not force and not needs_build():
+def build_library(force: bool = False, jobs: int = 8, extra_flags=(), lib: str = LIB) -> str:
+    """Build `lib`.  `extra_flags` (e.g. -DSNRSE_STAMPS for the timing-diagnostic build) go to
+    every compile; such builds use their own object directory next to `lib`."""
+    if lib == LIB and not force and not needs_build():
         return LIB
-    objdir = os.path.join(LIBDIR, "obj")
+    objdir = os.path.join(os.path.dirname(lib), "obj")
     os.makedirs(objdir, exist_ok=True)
     hdr_t = max([os.path.getmtime(h) for h in _headers()] + [0.0])
     todo, objs = [], []
@@ -56,15 +58,15 @@ def build_library(force: bool = False, jobs: int = 8) -> str:
         if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_t):
             todo.append((src, obj))
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo) or 1))) as ex:
-        for f in [ex.submit(_compile, s, o) for s, o in todo]:
+        for f in [ex.submit(_compile, s, o, tuple(extra_flags)) for s, o in todo]:
             f.result()
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     r = subprocess.run([HIPCC, "-shared", f"--offload-arch={ARCH}", *objs, "-o", tmp],
                        capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":

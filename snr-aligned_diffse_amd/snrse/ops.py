@@ -43,7 +43,7 @@ def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_w
            out_f32=False, stats=None, gn=None, gn_act=True):
     """NHWC conv (see snrse_conv2d).  src0 [B,H,W,C0]; returns out [B,H,W,cout].
     temb: [B, R] f32 table of all Dense_0 outputs, this layer's columns start at temb_off.
-    stats: optional [B, cout, 2] f64 tensor receiving the output's per-channel (sum, sumsq).
+    stats: optional new_stats() buffer receiving the output's per-channel (sum, sumsq).
     gn: optional (scale, shift) [B, C0+C1] f32 — consume SiLU(GN(x)) (halo path only, see halo_ok)."""
     _dev(src0, src1, wgt, sc, sc1, sc_wgt, bias, res, comb, comb_w, comb_b, temb)
     B, H, W, C0 = src0.shape
@@ -69,14 +69,14 @@ def halo_ok(x, ksize, cout):
     """True when snrse_conv2d takes the halo path (and so accepts a fused GroupNorm)."""
     B, H, W, C = x.shape
     return (x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and H % 4 == 0 and W % 64 == 0
-            and _VARIANT["v"] == 0 and x.numel() * 2 < 0x7ff00000)
+            and _VARIANT["v"] in (0, 4) and x.numel() * 2 < 0x7ff00000)
 
 
 def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):
     """Per-(b, c) GroupNorm affine [B, C] x 2 from per-channel sums."""
     _dev(sums0, sums1, gamma, beta)
-    B, C0 = sums0.shape[0], sums0.shape[1]
-    C1 = 0 if sums1 is None else sums1.shape[1]
+    B, C0 = sums0.shape[0], sums0.shape[2]
+    C1 = 0 if sums1 is None else sums1.shape[2]
     C = C0 + C1
     g = groups if groups is not None else min(C // 4, 32)
     scale = torch.empty(B, C, device=sums0.device, dtype=torch.float32)
@@ -86,13 +86,22 @@ def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):
     return scale, shift
 
 
+STAT_SLOTS = 16  # SNRSE_STAT_SLOTS (include/snrse.h)
+
+
 def new_stats(x_or_shape, C=None):
-    """Empty [B, C, 2] f64 per-channel statistics buffer for an NHWC tensor."""
+    """Empty [B, STAT_SLOTS, C, 2] f64 per-channel statistics buffer for an NHWC tensor
+    (producers spread their atomics over the slots; consumers fold them)."""
     if C is None:
         B, C, dev = x_or_shape.shape[0], x_or_shape.shape[-1], x_or_shape.device
     else:
         B, dev = x_or_shape, torch.device("cuda")
-    return torch.empty(B, C, 2, device=dev, dtype=torch.float64)
+    return torch.empty(B, STAT_SLOTS, C, 2, device=dev, dtype=torch.float64)
+
+
+def fold_stats(st):
+    """[B, STAT_SLOTS, C, 2] -> [B, C, 2] per-channel (sum, sumsq) (inspection / tests)."""
+    return st.sum(1)
 
 
 def gn_stats(src0, src1=None):
@@ -112,7 +121,7 @@ MODES = {"none": 0, "down": 1, "up": 2}
 
 def gn_apply(src0, src1=None, sums=None, gamma=None, beta=None, act=True, mode="none", groups=None, eps=1e-6,
              sums1=None):
-    """sums: per-channel stats of src0 ([B, C0, 2]) or a (sums0, sums1) pair; None = no norm."""
+    """sums: new_stats() buffer of src0 or a (sums0, sums1) pair; None = no norm."""
     if isinstance(sums, tuple):
         sums, sums1 = sums
     _dev(src0, src1, sums, sums1, gamma, beta)

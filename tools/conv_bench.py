@@ -55,6 +55,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--shapes", default="", help="comma list of SHAPES indices (default all)")
     a = ap.parse_args()
     dev = torch.device("cuda")
@@ -63,11 +64,13 @@ def main():
     for sh in sel:
         outs = {}
         row = {"shape": sh}
-        for v in [int(x) for x in a.variants.split(",")]:
-            out, ms, fl = run(sh, v, a.reps, dev)
-            outs[v] = out.float()
-            row[f"v{v}_ms"] = ms
-            row[f"v{v}_tflops"] = fl / ms / 1e9
+        for rnd in range(a.rounds):  # interleaved A/B rounds: clocks drift between launches
+            for v in [int(x) for x in a.variants.split(",")]:
+                out, ms, fl = run(sh, v, a.reps, dev)
+                outs[v] = out.float()
+                ms = min(ms, row.get(f"v{v}_ms", ms))
+                row[f"v{v}_ms"] = ms
+                row[f"v{v}_tflops"] = fl / ms / 1e9
         if len(outs) > 1:
             ks = list(outs)
             d = (outs[ks[0]] - outs[ks[1]]).abs().max().item()

@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Segment timeline of the halo conv kernel from the -DSNRSE_STAMPS diagnostic build.
+
+  python tools/conv_stamps.py --build          # here: builds lib/stamps/libsnrse_hip.so
+  python tools/conv_stamps.py [--shape 0]      # on the GPU box: prints per-segment shares
+
+Each wave records s_memtime at: kernel start (0), prologue done (1), per phase q the end of
+the phase-start wait+barrier (2+2q) and the end of its MFMA section (3+2q), epilogue start
+(28) and end (29).  The stamp build's run time is not the product's (stamps fence overlaps):
+read shares, not lengths.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "snr-aligned_diffse_amd")
+sys.path.insert(0, PKG)
+STAMP_LIB = os.path.join(PKG, "lib", "stamps", "libsnrse_hip.so")
+
+
+def build():
+    from snrse import build as b
+    os.makedirs(os.path.dirname(STAMP_LIB), exist_ok=True)
+    print(b.build_library(force=True, extra_flags=("-DSNRSE_STAMPS",), lib=STAMP_LIB))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--shapes", default="0")
+    ap.add_argument("--variants", default="0")
+    ap.add_argument("--stats", default="1", help="comma list of 0/1: fuse GN statistics")
+    a = ap.parse_args()
+    if a.build:
+        return build()
+    os.environ["SNRSE_LIB"] = STAMP_LIB
+    import numpy as np
+    import torch
+    from snrse import _lib, ops
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from conv_bench import SHAPES
+
+    lib = _lib.load()
+    lib.snrse_debug_set_stamps.argtypes = [ctypes.c_void_p]
+    dev = torch.device("cuda")
+    for si in [int(x) for x in a.shapes.split(",")]:
+        B, C0, C1, Co, H, W, k, Csc = SHAPES[si]
+        g = torch.Generator(device=dev).manual_seed(0)
+        x0 = torch.randn(B, H, W, C0, device=dev, generator=g).bfloat16()
+        x1 = torch.randn(B, H, W, C1, device=dev, generator=g).bfloat16() if C1 else None
+        sc = torch.randn(B, H, W, Csc, device=dev, generator=g).bfloat16() if Csc else None
+        w = (torch.randn(Co, k * k * (C0 + C1), device=dev, generator=g) / 30).bfloat16()
+        ws = (torch.randn(Co, Csc, device=dev, generator=g) / 16).bfloat16() if Csc else None
+        bias = torch.zeros(Co, device=dev)
+        nblk = B * (H // 4) * (W // 64) * (Co // 128)
+        buf = torch.zeros(nblk * 8 * 32, dtype=torch.int64, device=dev)
+        for v, use_st in [(int(x), int(y)) for x in a.variants.split(",") for y in a.stats.split(",")]:
+            ops.set_option("conv_variant", v)
+            st = ops.new_stats(B, Co) if use_st else None
+            lib.snrse_debug_set_stamps(None)
+            out = ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, stats=st)
+            for _ in range(3):
+                ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, out=out, stats=st)
+            buf.zero_()
+            lib.snrse_debug_set_stamps(buf.data_ptr())
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, out=out, stats=st)
+            e1.record()
+            torch.cuda.synchronize()
+            lib.snrse_debug_set_stamps(None)
+            ms = e0.elapsed_time(e1)
+            s = buf.view(nblk, 8, 32).cpu().numpy().astype(np.int64)
+            cin = C0 + C1
+            nq = 3 * (cin // 64) + (Csc // 64)
+            t0 = s[:, :, 0]
+            rel = s - t0[:, :, None]
+            seg = {"prologue": rel[:, :, 1]}
+            prev = rel[:, :, 1]
+            waits, comps = [], []
+            for q in range(nq):
+                waits.append(rel[:, :, 2 + 2 * q] - prev)
+                comps.append(rel[:, :, 3 + 2 * q] - rel[:, :, 2 + 2 * q])
+                prev = rel[:, :, 3 + 2 * q]
+            seg["tail_to_epi"] = rel[:, :, 28] - prev
+            seg["epilogue"] = rel[:, :, 29] - rel[:, :, 28]
+            res = {"shape": SHAPES[si], "variant": v, "stats": use_st, "ms": ms, "nq": nq,
+                   "wave_total_mean": float(rel[:, :, 29].mean())}
+            res.update({k_: float(v_.mean()) for k_, v_ in seg.items()})
+            res["wait_per_phase"] = [round(float(x.mean())) for x in waits]
+            res["mfma_per_phase"] = [round(float(x.mean())) for x in comps]
+            res["wait_per_phase_by_wave"] = [[round(float(x[:, wv].mean())) for wv in range(8)] for x in waits[:3]]
+            # gaps between consecutive blocks on one CU (dispatch + tail effects)
+            hw = s[:, 0, 30]
+            xcc = s[:, 0, 31]
+            cu = (xcc << 16) | (hw & 0xFF00)
+            start, end = s[:, :, 0].min(1), s[:, :, 29].max(1)
+            gaps = []
+            for key in np.unique(cu)[:64]:
+                idx = np.where(cu == key)[0]
+                o = idx[np.argsort(start[idx])]
+                if len(o) > 1:
+                    gaps.extend((start[o[1:]] - end[o[:-1]]).tolist())
+            res["block_lifetime_mean"] = float((end - start).mean())
+            res["inter_block_gap_median"] = float(np.median(gaps)) if gaps else None
+            res["blocks_per_cu_mean"] = float(nblk / len(np.unique(cu)))
+            print(json.dumps(res), flush=True)
+    ops.set_option("conv_variant", 0)
+
+
+if __name__ == "__main__":
+    main()
