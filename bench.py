@@ -95,7 +95,11 @@ def conv_flops(src0, src1, ksize, cout, sc, sc1):
 
 
 class ConvProbe:
-    """Per-launch HIP events on the launch stream around every big-tile conv GEMM launch."""
+    """HIP events on the launch stream around every launch of the dominant kernel — the halo
+    implicit-GEMM conv (bf16 3x3, Cout % 128 == 0, H % 4 == 0, W % 64 == 0; ops.halo_ok) —
+    during one extra enhance() pass after the timed region.  achieved = algorithmic FLOPs of
+    those launches / their summed event time, i.e. mean FLOPs per launch / mean launch
+    duration (the quantity rocprofv3 --stats reports as AverageNs for that kernel)."""
 
     def __init__(self):
         self.rec = []
@@ -105,7 +109,7 @@ class ConvProbe:
         probe = self
 
         def wrapped(src0, wgt, ksize, cout, *a, **kw):
-            if cout < 64:
+            if not ops.halo_ok(src0, ksize, cout):
                 return orig(src0, wgt, ksize, cout, *a, **kw)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -125,6 +129,19 @@ class ConvProbe:
         fl = sum(r[0] for r in self.rec)
         ms = sum(r[1].elapsed_time(r[2]) for r in self.rec)
         return fl, ms, len(self.rec)
+
+
+def pmc_traffic(kernel_prefix):
+    """HBM bytes per launch of the dominant kernel from the committed PMC profile
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950
+    correction + WRITE_SIZE); None when absent."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("kernel", "").startswith(kernel_prefix):
+            return d.get("bytes_per_launch"), os.path.relpath(path, ROOT)
+    return None, None
 
 
 def main():
@@ -184,11 +201,14 @@ def main():
         finally:
             probe.uninstall()
         fl, ms, n = probe.summary()
-        ach = fl / (ms * 1e-3)
+        ach = fl / (ms * 1e-3) if ms > 0 else 0.0
         peak = PEAK[args.dtype]
+        kname = ops.conv_kernel_name()
+        traffic, tsrc = pmc_traffic(kname)
         roof = {"bound": "mfma", "achieved": ach / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
-                "frac": ach / peak, "traffic": None, "kernel": "conv_mfma_kernel (big-tile GEMMs)",
-                "launches": n, "kernel_ms_per_step": ms}
+                "frac": ach / peak, "traffic": traffic, "kernel": kname, "launches_per_step": n,
+                "avg_launch_us": ms * 1e3 / max(n, 1), "flop_per_launch": fl / max(n, 1),
+                "kernel_ms_per_step": ms, "traffic_source": tsrc}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -86,8 +86,13 @@ int snrse_gn_apply(const void* src0, int C0, const void* src1, int C1, int B, in
                    const double* sums, const double* sums1, const float* gamma, const float* beta,
                    int groups, float eps, int act, int mode, void* out, int dtype, hipStream_t stream);
 
-/* Tuning switches (A/B experiments): "conv_variant" 0 auto, 1 register-staged v1, 2 LDS-DMA v2. */
+/* Tuning switches (A/B experiments): "conv_variant" 0 auto, 1 register-staged v1, 2 LDS-DMA v2,
+ * 4 halo kernel v4 with the register epilogue, 5 halo kernel v5 (two workgroups per CU). */
 int snrse_set_option(const char* name, int value);
+
+/* Read back a switch: "conv_variant", or "halo_kernel" = generation of the halo conv kernel
+ * the current setting dispatches to (4: conv_halo_kernel, 5: conv_halo5_kernel). */
+int snrse_get_option(const char* name, int* value);
 
 /* AttnBlockpp attention core (layerspp.py:84-88): qkv [B][L][3C] -> out [B][L][C],
  * softmax(q k^T / sqrt(C)) v, flash-style on MFMA.  C must be 256. */

@@ -23,6 +23,13 @@ SNRSE_DEV bf16_t f2bf(float f) {
   return (bf16_t)(u >> 16);
 }
 
+// two f32 -> packed bf16x2 with the hardware RNE convert (v_cvt_pk_bf16_f32; NaN stays NaN)
+SNRSE_DEV uint32_t pack_bf16x2(float lo, float hi) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+  const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
 template <typename T> struct Elem;
 template <> struct Elem<float> {
   static constexpr int kBytes = 4;
@@ -63,11 +70,11 @@ enum { SNRSE_F32 = 0, SNRSE_BF16 = 1 };
 // their atomics over the slots (a few hundred workgroups per image would otherwise queue on
 // the same 2*C addresses), consumers sum the slots.
 #define SNRSE_STAT_SLOTS 16
-SNRSE_DEV inline size_t stat_idx(int b, int slot, int c, int C) {
+SNRSE_DEV size_t stat_idx(int b, int slot, int c, int C) {
   return (((size_t)b * SNRSE_STAT_SLOTS + slot) * C + c) * 2;
 }
 // (sum, sumsq) of channel c of image b, folded over the slots
-SNRSE_DEV inline void stat_fold(const double* st, int b, int c, int C, double& s, double& ss) {
+SNRSE_DEV void stat_fold(const double* st, int b, int c, int C, double& s, double& ss) {
 #pragma unroll 4
   for (int k = 0; k < SNRSE_STAT_SLOTS; ++k) {
     const double* q = st + stat_idx(b, k, c, C);

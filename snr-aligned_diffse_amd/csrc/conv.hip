@@ -116,7 +116,23 @@ SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
 // When the whole block tile lies in one image (blk_b >= 0) the GN statistics are reduced over
 // the block's NWM wave rows in LDS (`red`, NWM x BN x 2 floats) and leave as one atomic pair per
 // channel per block; every wave of the block must call this (it holds a barrier then).
-template <typename TO, int NWM, int BN>
+// Block-level GN statistics flush: sum the NWM wave rows of `red` and add one (sum, sumsq)
+// pair per channel to the slotted stats buffer.  Holds a barrier (all waves call it).
+template <int NWM, int BN>
+SNRSE_DEV void block_stats_flush(const ConvParams& p, const float* red, int blk_b, int blk_n0) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const int slot = blockIdx.x & (SNRSE_STAT_SLOTS - 1);
+  for (int t = threadIdx.x; t < 2 * BN; t += blockDim.x) {
+    float a = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWM; ++w) a += red[w * 2 * BN + t];
+    if (blk_n0 + (t >> 1) < p.Cout)
+      unsafeAtomicAdd(&p.stats[stat_idx(blk_b, slot, blk_n0 + (t >> 1), p.Cout) + (t & 1)], (double)a);
+  }
+}
+
+template <typename TO, int NWM, int BN, bool DEFER = false>
 SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int mb, int nb, int lane, float* stage,
                             float* red, int wm, int blk_b, int blk_n0) {
   constexpr int LDR = 68;  // padded row (floats): conflict-free C-layout writes
@@ -229,14 +245,7 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
         red[(wm * BN + nb - blk_n0 + cc * EPC + k) * 2 + 1] = s2[k];
       }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    for (int t = threadIdx.x; t < 2 * BN; t += blockDim.x) {
-      float a = 0.f;
-#pragma unroll
-      for (int w = 0; w < NWM; ++w) a += red[w * 2 * BN + t];
-      if (blk_n0 + (t >> 1) < p.Cout) unsafeAtomicAdd(&p.stats[stat_idx(blk_b, slot, blk_n0 + (t >> 1), p.Cout) + (t & 1)], (double)a);
-    }
+    if constexpr (!DEFER) block_stats_flush<NWM, BN>(p, red, blk_b, blk_n0);
   } else if (p.stats && one_b && r0 == 0 && nok) {
     const size_t base = stat_idx(mb / HW, slot, n, p.Cout);
 #pragma unroll
@@ -244,6 +253,116 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
       unsafeAtomicAdd(&p.stats[base + 2 * k], (double)s1[k]);
       unsafeAtomicAdd(&p.stats[base + 2 * k + 1], (double)s2[k]);
     }
+  }
+}
+
+// Lean LDS-staged epilogue of the halo kernels: the wave's 64 rows are 64 consecutive pixels of
+// image `b` and its 64 channels are in range (H % 4 == 0, W % 64 == 0, Cout % 128 == 0 there), so
+// bias / temb / Combine weights are per-lane constants and no row or column masking is needed.
+template <typename TO, int NWM, int BN, bool DEFER>
+SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int mb, int nb, int lane, float* stage,
+                            float* red, int wm, int b, int blk_n0) {
+  constexpr int LDR = 68;
+  constexpr int EPC = 16 / (int)sizeof(TO);
+  constexpr int NCH = 64 / EPC;
+  constexpr int RPP = 64 / NCH;
+  const int lrow = lane & 15, lg = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) stage[(i * 16 + lg * 4 + e) * LDR + j * 16 + lrow] = acc[i][j][e];
+  const int cc = lane % NCH, r0 = lane / NCH;
+  const int n = nb + cc * EPC;
+  float add[EPC];
+#pragma unroll
+  for (int k = 0; k < EPC; ++k) add[k] = 0.f;
+  if (p.bias) {
+#pragma unroll
+    for (int k = 0; k < EPC; k += 4) {
+      const f32x4 v = *(const f32x4*)(p.bias + n + k);
+      add[k] += v[0]; add[k + 1] += v[1]; add[k + 2] += v[2]; add[k + 3] += v[3];
+    }
+  }
+  if (p.temb) {
+    const float* tb = p.temb + (size_t)b * p.temb_stride + n;
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) add[k] += tb[k];
+  }
+  float cw[EPC][4], cb[EPC];
+  if (p.comb_src) {
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) {
+      const f32x4 w = *(const f32x4*)(p.comb_w + (size_t)(n + k) * 4);
+      cw[k][0] = w[0]; cw[k][1] = w[1]; cw[k][2] = w[2]; cw[k][3] = w[3];
+      cb[k] = p.comb_b[n + k];
+    }
+  }
+  float s1[EPC], s2[EPC];
+#pragma unroll
+  for (int k = 0; k < EPC; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int pass = 0; pass < 64 / RPP; ++pass) {
+    const int row = r0 + pass * RPP;
+    const size_t m = (size_t)mb + row;
+    float v[EPC];
+    const float* sr = stage + row * LDR + cc * EPC;
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) v[k] = sr[k] + add[k];
+    if (p.res) {
+      const u32x4 rv = *(const u32x4*)((const TO*)p.res + m * p.res_ld + n);
+      if constexpr (sizeof(TO) == 2) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] += __uint_as_float(rv[k] << 16);
+          v[2 * k + 1] += __uint_as_float(rv[k] & 0xffff0000u);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] += __uint_as_float(rv[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) v[k] *= p.out_scale;
+    if (p.comb_src) {
+      const f32x4 q = *(const f32x4*)(p.comb_src + m * 4);
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) v[k] += q[0] * cw[k][0] + q[1] * cw[k][1] + q[2] * cw[k][2] + q[3] * cw[k][3] + cb[k];
+    }
+    u32x4 o;
+    if constexpr (sizeof(TO) == 2) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = pack_bf16x2(v[2 * k], v[2 * k + 1]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = __float_as_uint(v[k]);
+    }
+    *(u32x4*)((TO*)p.out + m * p.out_ld + n) = o;
+    if (p.stats) {
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) { s1[k] += v[k]; s2[k] = fmaf(v[k], v[k], s2[k]); }
+    }
+  }
+  if (p.stats) {
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) {
+#pragma unroll
+      for (int o = NCH; o < 64; o <<= 1) {
+        s1[k] += __shfl_xor(s1[k], o, 64);
+        s2[k] += __shfl_xor(s2[k], o, 64);
+      }
+    }
+    if (r0 == 0) {
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) {
+        red[(wm * BN + nb - blk_n0 + cc * EPC + k) * 2] = s1[k];
+        red[(wm * BN + nb - blk_n0 + cc * EPC + k) * 2 + 1] = s2[k];
+      }
+    }
+    if constexpr (!DEFER) block_stats_flush<NWM, BN>(p, red, b, blk_n0);
   }
 }
 
@@ -717,7 +836,7 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(ConvParams p) {
             lo = fmaf(lo, gsc[2 * i], gsh[2 * i]);
             hi = fmaf(hi, gsc[2 * i + 1], gsh[2 * i + 1]);
             if (p.gn_act) { lo = silu(lo); hi = silu(hi); }
-            v[i] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+            v[i] = pack_bf16x2(lo, hi);
           }
         } else {
           v = u32x4{0u, 0u, 0u, 0u};
@@ -807,8 +926,9 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(ConvParams p) {
   if constexpr (LDS_EPI) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // LDS is reused as the epilogue staging area
-    epilogue_lds<TO, 4, 128>(p, acc, (bb * p.H + h0 + wm) * p.W + w0, n0 + wn * 64, lane,
-                             (float*)(smem + wid * (64 * 68 * 4)), (float*)(smem + 8 * (64 * 68 * 4)), wm, bb, n0);
+    epilogue_img<TO, 4, 128, false>(p, acc, (bb * p.H + h0 + wm) * p.W + w0, n0 + wn * 64, lane,
+                                    (float*)(smem + wid * (64 * 68 * 4)), (float*)(smem + 8 * (64 * 68 * 4)), wm,
+                                    bb, n0);
   } else {
     epilogue<TO, FM, FN>(p, acc, (bb * p.H + h0 + wm) * p.W + w0, n0 + wn * 64, lane);
   }
@@ -849,6 +969,253 @@ int launch_halo(ConvParams p, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------
+// v5 halo GEMM, two workgroups per CU.  4 waves; tile = 4 image rows x 64 px x 128 couts; wave w
+// computes output row h0+w (64 px) x all 128 couts (acc 128 VGPRs).  K runs in 32-channel chunks:
+// halo 396 rows x 64 B (25 KB, register-staged with the fused GroupNorm+SiLU) + a 2-slot ring of
+// 3-tap weight phases (2 x 24 KB, LDS-DMA) = 72.75 KB, so two workgroups share a CU and one's
+// prologue / epilogue runs under the other's MFMAs (v4 is 1 workgroup/CU, 152 KB).
+SNRSE_DEV int swz64(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >> 1) & 3)) << 4); }
+
+template <typename TO>
+__global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
+  constexpr int TH = 4, TW = 64, HC = TW + 2;
+  constexpr int HROWS = (TH + 2) * HC;  // 396
+  constexpr int HJ = 7;                 // halo rows per thread: (tid >> 2) + 64 j
+  constexpr int HALO_BYTES = HROWS * 64;
+  constexpr int TAPB = 128 * 64;  // one tap's 128 couts x 32 ch bf16
+  constexpr int SLOT = 3 * TAPB;
+  constexpr int KT = 32;
+  static_assert(64 * HJ >= HROWS, "halo rows");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const halo = smem;
+  char* const ring = smem + HALO_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef SNRSE_STAMPS
+  unsigned long long* const lst = (unsigned long long*)(ring + 2 * SLOT) + wid * 32;
+#endif
+  SNRSE_STAMP(0);
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7, pos = bid >> 3;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
+  const int n0 = (wg % p.ntn) * 128;
+  int tile = wg / p.ntn;
+  const int ntw = p.W / TW, nth = p.H / TH;
+  const int w0 = (tile % ntw) * TW;
+  tile /= ntw;
+  const int h0 = (tile % nth) * TH;
+  const int bb = tile / nth;
+
+  const int Cin = p.C0 + p.C1;
+  const int cbm = Cin / KT;
+  const int Csc_all = p.Csc + p.Csc1;
+  const int cbs = p.sc_src ? Csc_all / KT : 0;
+  const int ncb = cbm + cbs;
+  const int nq = 3 * cbm + cbs;
+  const int K1 = 9 * Cin;
+  const int hcol = tid & 3;  // this thread's 16-B chunk (8 channels) of its halo rows
+  const bool gn = p.gn_scale != nullptr;
+
+  int hpix[HJ];
+  bool hok[HJ];
+#pragma unroll
+  for (int j = 0; j < HJ; ++j) {
+    const int hr = (tid >> 2) + 64 * j;
+    const int hy = hr / HC, hx = hr - (hr / HC) * HC;
+    const int ih = h0 + hy - 1, iw = w0 + hx - 1;
+    hok[j] = hr < HROWS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+    hpix[j] = (bb * p.H + ih) * p.W + iw;
+  }
+
+  u32x4 hv[HJ];
+  float gsc[8], gsh[8];
+
+#define SNRSE_HALO5_LOADS(BASE_, BYTES_, CS_, CC_)                                                     \
+  do {                                                                                              \
+    const __amdgpu_buffer_rsrc_t r_ = make_rsrc((BASE_), (BYTES_));                                 \
+    const int cs_ = (CS_), cc_ = (CC_) + hcol * 8;                                                  \
+    _Pragma("unroll") for (int j = 0; j < HJ; ++j) {                                                \
+      const int voff_ = hok[j] ? (hpix[j] * cs_ + cc_) * 2 : (int)0x80000000;                       \
+      hv[j] = __builtin_amdgcn_raw_buffer_load_b128(r_, voff_, 0, 0);                               \
+    }                                                                                               \
+  } while (0)
+  auto halo_load = [&](int c) {
+    if (c < cbm) {
+      const int ch = c * KT;
+      if (ch < p.C0) SNRSE_HALO5_LOADS(p.src0, p.bytes0, p.C0, ch);
+      else SNRSE_HALO5_LOADS(p.src1, p.bytes1, p.C1, ch - p.C0);
+      if (gn) {
+        const float* sp = p.gn_scale + (size_t)bb * Cin + ch + hcol * 8;
+        const float* hp = p.gn_shift + (size_t)bb * Cin + ch + hcol * 8;
+        const f32x4 s0 = *(const f32x4*)sp, s1 = *(const f32x4*)(sp + 4);
+        const f32x4 t0 = *(const f32x4*)hp, t1 = *(const f32x4*)(hp + 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { gsc[i] = s0[i]; gsc[4 + i] = s1[i]; gsh[i] = t0[i]; gsh[4 + i] = t1[i]; }
+      }
+    } else {
+      const int ch = (c - cbm) * KT;
+      if (ch < p.Csc) SNRSE_HALO5_LOADS(p.sc_src, p.sc_bytes0, p.Csc, ch);
+      else SNRSE_HALO5_LOADS(p.sc_src1, p.sc_bytes1, p.Csc1, ch - p.Csc);
+    }
+  };
+#undef SNRSE_HALO5_LOADS
+  auto halo_store = [&](int c) {
+    const bool tr = gn && c < cbm;
+#pragma unroll
+    for (int j = 0; j < HJ; ++j) {
+      const int hr = (tid >> 2) + 64 * j;
+      if (j == HJ - 1 && hr >= HROWS) break;
+      u32x4 v = hv[j];
+      if (tr) {
+        if (hok[j]) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float lo = __uint_as_float(v[i] << 16), hi = __uint_as_float(v[i] & 0xffff0000u);
+            lo = fmaf(lo, gsc[2 * i], gsh[2 * i]);
+            hi = fmaf(hi, gsc[2 * i + 1], gsh[2 * i + 1]);
+            if (p.gn_act) { lo = silu(lo); hi = silu(hi); }
+            v[i] = pack_bf16x2(lo, hi);
+          }
+        } else {
+          v = u32x4{0u, 0u, 0u, 0u};
+        }
+      }
+      *(u32x4*)(halo + swz64(hr, hcol)) = v;
+    }
+  };
+  // weights of phase q -> ring slot q & 1: nt taps x 8 pieces of 1 KB (16 rows x 64 B), lane-
+  // linear LDS destination, swizzle applied on the source chunk.
+  auto wload = [&](int q) {
+    int c, t0, nt;
+    if (q < 3 * cbm) { c = q / 3; t0 = (q - c * 3) * 3; nt = 3; }
+    else { c = cbm + (q - 3 * cbm); t0 = 4; nt = 1; }
+    const bool mainw = c < cbm;
+    const int wld = mainw ? K1 : Csc_all;
+    const int kb = mainw ? c * KT : (c - cbm) * KT;
+    const __amdgpu_buffer_rsrc_t r = mainw ? make_rsrc(p.wgt, p.wbytes) : make_rsrc(p.sc_wgt, p.sc_wbytes);
+    char* dst = ring + (q & 1) * SLOT;
+    const int rl = lane >> 2, sl = lane & 3;
+    for (int ii = wid; ii < nt * 8; ii += 4) {
+      const int jt = ii >> 3, pc = ii & 7;
+      const int koff = mainw ? (t0 + jt) * Cin + kb : kb;
+      const int row = pc * 16 + rl;
+      const unsigned voff = (unsigned)(((n0 + row) * wld + koff + (sl ^ ((row >> 1) & 3)) * 8) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          r, (__attribute__((address_space(3))) void*)(dst + jt * TAPB + pc * 1024), 16, voff, 0, 0, 0);
+    }
+  };
+
+  f32x4 acc[2][4][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  halo_load(0);
+  wload(0);
+  halo_store(0);
+  SNRSE_STAMP(1);
+  const int lrow = lane & 15, lg = lane >> 4;
+  bool halo_inflight = false;
+  for (int q = 0; q < nq; ++q) {
+    int c, t0, nt;
+    if (q < 3 * cbm) { c = q / 3; t0 = (q - c * 3) * 3; nt = 3; }
+    else { c = cbm + (q - 3 * cbm); t0 = 4; nt = 1; }
+    const bool first = c < cbm ? t0 == 0 : true;
+    const bool last = c < cbm ? t0 == 6 : true;
+    // the halo prefetch issued after the previous phase's weights may stay in flight
+    if (halo_inflight) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    SNRSE_STAMP(2 + 2 * (q & 15));
+    if (q + 1 < nq) wload(q + 1);
+    halo_inflight = false;
+    if (first && c + 1 < ncb) {
+      halo_load(c + 1);
+      halo_inflight = !last && q + 1 < nq;
+    }
+    const char* sl = ring + (q & 1) * SLOT;
+    for (int jt = 0; jt < nt; ++jt) {
+      const int tp = t0 + jt;
+      const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
+      const int hbase = (wid + dy + 1) * HC + dx + 1 + lrow;
+      const char* sb = sl + jt * TAPB;
+      u32x4 af[4], bfr[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *(const u32x4*)(halo + swz64(hbase + i * 16, lg));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bfr[j] = *(const u32x4*)(sb + swz64(j * 16 + lrow, lg));
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[h][i][j] = mfma_chunk<bf16_t>(af[i], bfr[h * 4 + j], acc[h][i][j]);
+    }
+    SNRSE_STAMP(3 + 2 * (q & 15));
+    if (last && c + 1 < ncb) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave is done reading halo(c)
+      halo_store(c + 1);
+    }
+  }
+  SNRSE_STAMP(28);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // LDS is reused as the epilogue staging area
+  float* const stage = (float*)(smem + wid * (64 * 68 * 4));
+  float* const red = (float*)(smem + 4 * (64 * 68 * 4));
+  const int mrow = (bb * p.H + h0 + wid) * p.W + w0;
+  epilogue_img<TO, 4, 128, true>(p, acc[0], mrow, n0, lane, stage, red, wid, bb, n0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  SNRSE_STAMP(26);
+  epilogue_img<TO, 4, 128, true>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0);
+  SNRSE_STAMP(27);
+  if (p.stats) block_stats_flush<4, 128>(p, red, bb, n0);
+#ifdef SNRSE_STAMPS
+  {
+    unsigned long long st_[29];
+    if (lane == 0)
+      for (int i = 0; i < 29; ++i) st_[i] = lst[i];
+    unsigned long long t_end;
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_end)::"memory");
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (lane == 0 && p.stamps) {
+      unsigned long long* g = p.stamps + ((size_t)blockIdx.x * 8 + wid) * 32;
+      for (int i = 0; i < 29; ++i) g[i] = st_[i];
+      g[29] = t_end;
+      g[30] = hw;
+      g[31] = xcc;
+    }
+  }
+#endif
+}
+
+template <typename TO>
+int launch_halo5(ConvParams p, hipStream_t s) {
+#ifdef SNRSE_STAMPS
+  constexpr size_t lds = 396 * 64 + 2 * 3 * 128 * 64 + 4 * 32 * 8;
+#else
+  constexpr size_t lds = 396 * 64 + 2 * 3 * 128 * 64;
+#endif
+  static bool attr = false;
+  if (!attr) {
+    SNRSE_RET(hipFuncSetAttribute((const void*)conv_halo5_kernel<TO>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds));
+    attr = true;
+  }
+  p.ntn = p.Cout / 128;
+  const int tiles = p.B * (p.H / 4) * (p.W / 64);
+  hipLaunchKernelGGL((conv_halo5_kernel<TO>), dim3(tiles * p.ntn), dim3(256), lds, s, p);
+  return (int)hipGetLastError();
+}
+
 template <typename T, typename TO, int BM, int BN, int WM, int WN>
 int launch_conv(ConvParams p, int npad, hipStream_t s) {
   p.ntn = npad / BN;
@@ -873,7 +1240,8 @@ int launch_glds(ConvParams p, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int g_conv_variant = 0;  // 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 4 halo w/ scalar epilogue
+int g_conv_variant = 0;  // 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 4 halo w/ scalar epilogue, 5 halo v5
+constexpr int kHaloAuto = 4;  // halo kernel generation taken by variant 0
 
 template <typename T, typename TO>
 int dispatch_conv(const ConvParams& p, hipStream_t s) {
@@ -883,8 +1251,10 @@ int dispatch_conv(const ConvParams& p, hipStream_t s) {
       const bool fits = p.bytes0 < 0x7ff00000ll && p.bytes1 < 0x7ff00000ll && p.sc_bytes0 < 0x7ff00000ll &&
                         p.sc_bytes1 < 0x7ff00000ll;
       if (g_conv_variant != 1 && fits) {
-        if (g_conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0)
+        if (g_conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0) {
+          if (g_conv_variant == 5 || (g_conv_variant == 0 && kHaloAuto == 5)) return launch_halo5<TO>(p, s);
           return g_conv_variant == 4 ? launch_halo<TO, false>(p, s) : launch_halo<TO, true>(p, s);
+        }
         if (p.gn_scale) return SNRSE_EINVAL;  // fused GroupNorm exists only on the halo path
         if (p.Cout % 256 == 0) return launch_glds<128, 256, TO>(p, s);
         return launch_glds<256, 128, TO>(p, s);
@@ -955,6 +1325,22 @@ extern "C" int snrse_debug_set_stamps(void* buf) {
   return 0;
 }
 #endif
+
+static bool name_is(const char* a, const char* b) {
+  int i = 0;
+  while (a[i] && a[i] == b[i]) ++i;
+  return a[i] == 0 && b[i] == 0;
+}
+
+extern "C" int snrse_get_option(const char* name, int* value) {
+  if (!name || !value) return SNRSE_EINVAL;
+  if (name_is(name, "conv_variant")) { *value = g_conv_variant; return 0; }
+  if (name_is(name, "halo_kernel")) {
+    *value = (g_conv_variant == 5 || (g_conv_variant == 0 && kHaloAuto == 5)) ? 5 : 4;
+    return 0;
+  }
+  return SNRSE_EINVAL;
+}
 
 extern "C" int snrse_set_option(const char* name, int value) {
   if (!name) return SNRSE_EINVAL;

@@ -29,6 +29,7 @@ SIGNATURES = {
     "snrse_gn_stats": [_vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _vp],
     "snrse_gn_apply": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _f, _i, _i, _vp, _i, _vp],
     "snrse_set_option": [C.c_char_p, _i],
+    "snrse_get_option": [C.c_char_p, _vp],
     "snrse_attention": [_vp, _vp, _i, _i, _i, _i, _vp],
     "snrse_temb_mlp": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp],
     "snrse_temb_dense": [_vp, _vp, _vp, _vp, _i, _i, _i, _vp],

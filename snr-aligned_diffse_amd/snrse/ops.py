@@ -4,6 +4,7 @@ Every op requires HIP device tensors and raises otherwise — there is no CPU fa
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 
 import torch
@@ -65,11 +66,22 @@ def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_w
 _VARIANT = {"v": 0}
 
 
+def get_option(name):
+    v = C.c_int(0)
+    _lib.call("snrse_get_option", name.encode(), C.addressof(v))
+    return v.value
+
+
+def conv_kernel_name():
+    """Kernel symbol the halo-eligible convs dispatch to under the current setting."""
+    return "conv_halo5_kernel" if get_option("halo_kernel") == 5 else "conv_halo_kernel"
+
+
 def halo_ok(x, ksize, cout):
     """True when snrse_conv2d takes the halo path (and so accepts a fused GroupNorm)."""
     B, H, W, C = x.shape
     return (x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and H % 4 == 0 and W % 64 == 0
-            and _VARIANT["v"] in (0, 4) and x.numel() * 2 < 0x7ff00000)
+            and _VARIANT["v"] in (0, 4, 5) and x.numel() * 2 < 0x7ff00000)
 
 
 def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):

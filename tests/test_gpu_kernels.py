@@ -33,12 +33,13 @@ def nchw(x):
 DT = {"f32": (torch.float32, 2e-6), "bf16": (torch.bfloat16, 1e-2)}
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 5])
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 16), (1, 256, 128, 4, 8), (3, 128, 256, 5, 7), (2, 384, 256, 4, 4),
                                    (2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (1, 256, 256, 12, 64)])
 def test_conv3x3(gpu, dt, shape, variant):
-    """variant: 0 auto (halo kernel where H%4==0, W%64==0), 1 register-staged, 2 LDS-DMA im2col."""
+    """variant: 0 auto (halo kernel where H%4==0, W%64==0), 1 register-staged, 2 LDS-DMA im2col,
+    4 halo v4 with the register epilogue, 5 halo v5 (two workgroups per CU)."""
     from snrse import ops
     dtype, tol = DT[dt]
     B, cin, cout, H, W = shape
@@ -60,9 +61,10 @@ def test_conv3x3(gpu, dt, shape, variant):
     assert rel(nchw(out.float()), ref) < tol
 
 
+@pytest.mark.parametrize("variant", [0, 4, 5])
 @pytest.mark.parametrize("hw", [(8, 8), (8, 64)])
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
-def test_conv_epilogue_shortcut_temb_comb(gpu, dt, hw):
+def test_conv_epilogue_shortcut_temb_comb(gpu, dt, hw, variant):
     """Conv_1 + Conv_2 shortcut as extra K, temb bias, residual scale, Combine term, fused stats."""
     from snrse import ops
     dtype, tol = DT[dt]
@@ -83,10 +85,16 @@ def test_conv_epilogue_shortcut_temb_comb(gpu, dt, hw):
            + temb[:, 20:20 + cout, None, None].double()) / math.sqrt(2)
     ref = ref + torch.einsum("bihw,oi->bohw", pyr.double(), cw.double()) + cb.double()[None, :, None, None]
     st = ops.new_stats(B, cout)
-    out = ops.conv2d(nhwc(h).to(gpu, dtype), w1.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu, dtype).contiguous(),
-                     3, cout, bias=b1.to(gpu), sc=nhwc(xs).to(gpu, dtype),
-                     sc_wgt=w2.reshape(cout, cin).to(gpu, dtype).contiguous(), temb=temb.to(gpu), temb_off=20,
-                     out_scale=1 / math.sqrt(2), comb=nhwc(pyr).to(gpu), comb_w=cw.to(gpu), comb_b=cb.to(gpu), stats=st)
+    ops.set_option("conv_variant", variant)
+    try:
+        out = ops.conv2d(nhwc(h).to(gpu, dtype),
+                         w1.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu, dtype).contiguous(),
+                         3, cout, bias=b1.to(gpu), sc=nhwc(xs).to(gpu, dtype),
+                         sc_wgt=w2.reshape(cout, cin).to(gpu, dtype).contiguous(), temb=temb.to(gpu), temb_off=20,
+                         out_scale=1 / math.sqrt(2), comb=nhwc(pyr).to(gpu), comb_w=cw.to(gpu), comb_b=cb.to(gpu),
+                         stats=st)
+    finally:
+        ops.set_option("conv_variant", 0)
     assert rel(nchw(out.float()), ref) < tol
     o = out.double()
     st_ref = torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)
@@ -315,7 +323,8 @@ def test_philox_noise_statistics(gpu):
 
 
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (2, 256, 128, 4, 64)])
-def test_conv_fused_groupnorm_silu(gpu, shape):
+@pytest.mark.parametrize("variant", [0, 5])
+def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     """Halo GEMM consuming SiLU(GN(x)) from raw x + per-(b,c) scale/shift (+ raw 1x1 shortcut)."""
     from snrse import ops
     B, cin, cout, H, W = shape
@@ -333,7 +342,11 @@ def test_conv_fused_groupnorm_silu(gpu, shape):
     sums = ops.gn_stats(s0, s1)
     gn = ops.gn_scale_shift(sums[0], g.to(gpu), be.to(gpu), H * W, sums1=sums[1])
     assert ops.halo_ok(s0, 3, cout)
-    out = ops.conv2d(s0, w.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu, torch.bfloat16).contiguous(), 3, cout,
-                     src1=s1, gn=gn, sc=nhwc(xs).to(gpu, torch.bfloat16),
-                     sc_wgt=w2.reshape(cout, 128).to(gpu, torch.bfloat16).contiguous())
+    ops.set_option("conv_variant", variant)
+    try:
+        out = ops.conv2d(s0, w.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu, torch.bfloat16).contiguous(), 3,
+                         cout, src1=s1, gn=gn, sc=nhwc(xs).to(gpu, torch.bfloat16),
+                         sc_wgt=w2.reshape(cout, 128).to(gpu, torch.bfloat16).contiguous())
+    finally:
+        ops.set_option("conv_variant", 0)
     assert rel(nchw(out.float()), ref) < 1e-2

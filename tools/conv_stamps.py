@@ -74,8 +74,10 @@ def main():
             lib.snrse_debug_set_stamps(None)
             ms = e0.elapsed_time(e1)
             s = buf.view(nblk, 8, 32).cpu().numpy().astype(np.int64)
+            s = s[:, :4] if v == 5 else s  # v5 workgroups have 4 waves
             cin = C0 + C1
-            nq = 3 * (cin // 64) + (Csc // 64)
+            kt = 32 if v == 5 else 64
+            nq = 3 * (cin // kt) + (Csc // kt)
             t0 = s[:, :, 0]
             rel = s - t0[:, :, None]
             seg = {"prologue": rel[:, :, 1]}
@@ -87,12 +89,16 @@ def main():
                 prev = rel[:, :, 3 + 2 * q]
             seg["tail_to_epi"] = rel[:, :, 28] - prev
             seg["epilogue"] = rel[:, :, 29] - rel[:, :, 28]
+            if v == 5:  # finer epilogue stamps: 26 after half 0, 27 after half 1 (before the stats flush)
+                seg["epi_half0"] = rel[:, :, 26] - rel[:, :, 28]
+                seg["epi_half1"] = rel[:, :, 27] - rel[:, :, 26]
+                seg["epi_flush_store"] = rel[:, :, 29] - rel[:, :, 27]
             res = {"shape": SHAPES[si], "variant": v, "stats": use_st, "ms": ms, "nq": nq,
                    "wave_total_mean": float(rel[:, :, 29].mean())}
             res.update({k_: float(v_.mean()) for k_, v_ in seg.items()})
             res["wait_per_phase"] = [round(float(x.mean())) for x in waits]
             res["mfma_per_phase"] = [round(float(x.mean())) for x in comps]
-            res["wait_per_phase_by_wave"] = [[round(float(x[:, wv].mean())) for wv in range(8)] for x in waits[:3]]
+            res["wait_per_phase_by_wave"] = [[round(float(x[:, wv].mean())) for wv in range(s.shape[1])] for x in waits[:3]]
             # gaps between consecutive blocks on one CU (dispatch + tail effects)
             hw = s[:, 0, 30]
             xcc = s[:, 0, 31]
