@@ -96,7 +96,7 @@ def conv_flops(src0, src1, ksize, cout, sc, sc1):
 
 class ConvProbe:
     """HIP events on the launch stream around every launch of the dominant kernel — the halo
-    implicit-GEMM conv (bf16 3x3, Cout % 128 == 0, H % 4 == 0, W % 64 == 0; ops.halo_ok) —
+    implicit-GEMM conv (bf16 3x3, Cout % 128 == 0, H % 4 == 0, W % 64 == 0, no Combine term; ops.halo_ok) —
     during one extra enhance() pass after the timed region.  achieved = algorithmic FLOPs of
     those launches / their summed event time, i.e. mean FLOPs per launch / mean launch
     duration (the quantity rocprofv3 --stats reports as AverageNs for that kernel)."""
@@ -109,7 +109,7 @@ class ConvProbe:
         probe = self
 
         def wrapped(src0, wgt, ksize, cout, *a, **kw):
-            if not ops.halo_ok(src0, ksize, cout):
+            if not ops.halo_ok(src0, ksize, cout) or kw.get("comb") is not None:
                 return orig(src0, wgt, ksize, cout, *a, **kw)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -155,6 +155,7 @@ def main():
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--conv-variant", type=int, default=0, help="snrse conv_variant option (0 = auto)")
     args = ap.parse_args()
 
     from snrse import dist as sdist
@@ -166,6 +167,7 @@ def main():
     from snrse import ncsnpp, ops, sampler
     from snrse.enhance import PCEnhancer
 
+    ops.set_option("conv_variant", args.conv_variant)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     net = ncsnpp.NCSNppHIP(formula_weights(), dtype=dtype, device=dev)
     enh = PCEnhancer(net, sampler.SDESpec("ouve", theta=1.5, sigma_min=0.05, sigma_max=0.5), N=args.N)

@@ -19,91 +19,12 @@
 // rows of 128 B, chunk' = chunk ^ (row & 7): conflict-free for the ds_read_b128 lane groups
 // of ANY 16 consecutive rows (each group's rows cover all residues mod 8), which the halo
 // kernel needs because its fragments start at arbitrary (tap-shifted) rows.
-#include "common.h"
+#include "conv_common.h"
+
+using namespace snrse_conv;
 
 namespace {
 
-template <typename T> struct ConvTraits;
-template <> struct ConvTraits<bf16_t> {
-  static constexpr int KT = 64;  // elements per K-tile (128 B)
-  static constexpr int EPC = 8;  // elements per 16-B chunk
-};
-template <> struct ConvTraits<float> {
-  static constexpr int KT = 32;
-  static constexpr int EPC = 4;
-};
-
-struct ConvParams {
-  const void* src0; int C0;
-  const void* src1; int C1;
-  int B, H, W;
-  int ksize;
-  const void* wgt;  // [Npad][ksize*ksize*Cin]
-  const void* sc_src; int Csc;    // shortcut source(s): [M][Csc] (+ [M][Csc1])
-  const void* sc_src1; int Csc1;
-  const void* sc_wgt;  // [Npad][Csc + Csc1]
-  const float* bias;   // [Cout]
-  const float* temb; int temb_stride;  // [B][temb_stride] (pre-offset to this layer's column 0)
-  const void* res; int res_ld;         // residual [M][res_ld] (same dtype as output)
-  float out_scale;
-  const float* comb_src;  // [M][4] f32 input-skip pyramid (Combine.Conv_0 input)
-  const float* comb_w;    // [Cout][4]
-  const float* comb_b;    // [Cout]
-  void* out; int Cout; int out_ld;
-  double* stats;  // optional [B][SLOTS][Cout][2] per-channel (sum, sumsq) of the output (zeroed by launcher)
-  int M;
-  int ntn;        // N tiles (v2 grid)
-  long long bytes0, bytes1, sc_bytes0, sc_bytes1, wbytes, sc_wbytes;  // buffer extents (v2)
-  const float* gn_scale;  // optional [B][Cin] GroupNorm scale/shift applied to the main input (halo path)
-  const float* gn_shift;
-  int gn_act;             // SiLU after the GroupNorm affine
-  unsigned long long* stamps;  // timing-diagnostic build only (-DSNRSE_STAMPS): [blocks][8][32]
-};
-
-#ifdef SNRSE_STAMPS
-// Diagnostic build: s_memtime stamps of the halo kernel's segments (LDS, copied out at the
-// end).  Read their shares, never the build's run time (the stamp waits forbid overlaps).
-unsigned long long* g_stamp_buf = nullptr;
-#define SNRSE_STAMP(I)                                                                        \
-  do {                                                                                      \
-    __builtin_amdgcn_sched_barrier(0);                                                      \
-    unsigned long long t_;                                                                  \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
-    __builtin_amdgcn_sched_barrier(0);                                                      \
-    if (lane == 0) lst[(I)] = t_;                                                           \
-  } while (0)
-#else
-#define SNRSE_STAMP(I) \
-  do {                 \
-  } while (0)
-#endif
-
-template <typename T>
-SNRSE_DEV f32x4 mfma_chunk(const u32x4& a, const u32x4& b, f32x4 acc);
-
-template <>
-SNRSE_DEV f32x4 mfma_chunk<bf16_t>(const u32x4& a, const u32x4& b, f32x4 acc) {
-  bf16x8_mfma av = __builtin_bit_cast(bf16x8_mfma, a);
-  bf16x8_mfma bv = __builtin_bit_cast(bf16x8_mfma, b);
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
-}
-template <>
-SNRSE_DEV f32x4 mfma_chunk<float>(const u32x4& a, const u32x4& b, f32x4 acc) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[j]), __uint_as_float(b[j]), acc, 0, 0, 0);
-  return acc;
-}
-
-SNRSE_DEV int swz(int row, int chunk) { return (row << 7) + ((chunk ^ (row & 7)) << 4); }
-
-SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
-  const uint64_t a = (uint64_t)base;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  const int n = __builtin_amdgcn_readfirstlane((int)bytes);
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
-}
 
 // Shared epilogue: y = (acc + bias + temb + res) * out_scale + combine; optional GroupNorm
 // statistics of y (per (b, channel) sum / sumsq) for the consumer's GroupNorm.
@@ -1240,8 +1161,8 @@ int launch_glds(ConvParams p, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int g_conv_variant = 0;  // 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 4 halo w/ scalar epilogue, 5 halo v5
-constexpr int kHaloAuto = 4;  // halo kernel generation taken by variant 0
+int g_conv_variant = 0;  // 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 4 halo w/ scalar epilogue, 5 halo v5, 6 persistent halo v6 (falls back to v4 outside its contract)
+constexpr int kHaloAuto = 5;  // halo kernel generation taken by variant 0 (fastest measured: profiles/)
 
 template <typename T, typename TO>
 int dispatch_conv(const ConvParams& p, hipStream_t s) {
@@ -1252,6 +1173,10 @@ int dispatch_conv(const ConvParams& p, hipStream_t s) {
                         p.sc_bytes1 < 0x7ff00000ll;
       if (g_conv_variant != 1 && fits) {
         if (g_conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0) {
+          if constexpr (sizeof(TO) == 2) {
+            if ((g_conv_variant == 6 || (g_conv_variant == 0 && kHaloAuto == 6)) && halo6_ok(p))
+              return launch_halo6(p, s);
+          }
           if (g_conv_variant == 5 || (g_conv_variant == 0 && kHaloAuto == 5)) return launch_halo5<TO>(p, s);
           return g_conv_variant == 4 ? launch_halo<TO, false>(p, s) : launch_halo<TO, true>(p, s);
         }
@@ -1335,8 +1260,9 @@ static bool name_is(const char* a, const char* b) {
 extern "C" int snrse_get_option(const char* name, int* value) {
   if (!name || !value) return SNRSE_EINVAL;
   if (name_is(name, "conv_variant")) { *value = g_conv_variant; return 0; }
-  if (name_is(name, "halo_kernel")) {
-    *value = (g_conv_variant == 5 || (g_conv_variant == 0 && kHaloAuto == 5)) ? 5 : 4;
+  if (name_is(name, "halo_kernel")) {  // generation taken by a halo-eligible bf16 conv
+    const int v = g_conv_variant == 0 ? kHaloAuto : g_conv_variant;
+    *value = (v == 6 || v == 5) ? v : 4;
     return 0;
   }
   return SNRSE_EINVAL;

@@ -74,14 +74,14 @@ def get_option(name):
 
 def conv_kernel_name():
     """Kernel symbol the halo-eligible convs dispatch to under the current setting."""
-    return "conv_halo5_kernel" if get_option("halo_kernel") == 5 else "conv_halo_kernel"
+    return {6: "conv_halo6_kernel", 5: "conv_halo5_kernel"}.get(get_option("halo_kernel"), "conv_halo_kernel")
 
 
 def halo_ok(x, ksize, cout):
     """True when snrse_conv2d takes the halo path (and so accepts a fused GroupNorm)."""
     B, H, W, C = x.shape
     return (x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and H % 4 == 0 and W % 64 == 0
-            and _VARIANT["v"] in (0, 4, 5) and x.numel() * 2 < 0x7ff00000)
+            and _VARIANT["v"] in (0, 4, 5, 6) and x.numel() * 2 < 0x7ff00000)
 
 
 def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):
@@ -91,8 +91,10 @@ def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):
     C1 = 0 if sums1 is None else sums1.shape[2]
     C = C0 + C1
     g = groups if groups is not None else min(C // 4, 32)
-    scale = torch.empty(B, C, device=sums0.device, dtype=torch.float32)
-    shift = torch.empty_like(scale)
+    # one [2, B, C] allocation: the persistent halo GEMM fetches scale and shift through a single
+    # buffer resource (shift == scale + B*C)
+    ss = torch.empty(2, B, C, device=sums0.device, dtype=torch.float32)
+    scale, shift = ss[0], ss[1]
     _lib.call("snrse_gn_scale_shift", sums0.data_ptr(), C0, _ptr(sums1), C1, B, HW, gamma.data_ptr(), beta.data_ptr(),
               g, float(eps), scale.data_ptr(), shift.data_ptr(), _stream())
     return scale, shift

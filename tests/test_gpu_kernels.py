@@ -33,13 +33,14 @@ def nchw(x):
 DT = {"f32": (torch.float32, 2e-6), "bf16": (torch.bfloat16, 1e-2)}
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 4, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 5, 6])
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 16), (1, 256, 128, 4, 8), (3, 128, 256, 5, 7), (2, 384, 256, 4, 4),
                                    (2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (1, 256, 256, 12, 64)])
 def test_conv3x3(gpu, dt, shape, variant):
-    """variant: 0 auto (halo kernel where H%4==0, W%64==0), 1 register-staged, 2 LDS-DMA im2col,
-    4 halo v4 with the register epilogue, 5 halo v5 (two workgroups per CU)."""
+    """variant: 0 auto (persistent halo kernel where H%4==0, W%64==0), 1 register-staged, 2 LDS-DMA
+    im2col, 4 halo v4 with the register epilogue, 5 halo v5 (two workgroups per CU), 6 persistent
+    halo v6 (falls back to v4 outside its contract)."""
     from snrse import ops
     dtype, tol = DT[dt]
     B, cin, cout, H, W = shape
@@ -323,7 +324,7 @@ def test_philox_noise_statistics(gpu):
 
 
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (2, 256, 128, 4, 64)])
-@pytest.mark.parametrize("variant", [0, 5])
+@pytest.mark.parametrize("variant", [0, 4, 5])
 def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     """Halo GEMM consuming SiLU(GN(x)) from raw x + per-(b,c) scale/shift (+ raw 1x1 shortcut)."""
     from snrse import ops
@@ -350,3 +351,66 @@ def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     finally:
         ops.set_option("conv_variant", 0)
     assert rel(nchw(out.float()), ref) < 1e-2
+
+
+@pytest.mark.parametrize("case", [
+    # B, C0, C1, Cout, H, W, Csc, Csc1, gn, temb, res, stats
+    (4, 128, 0, 128, 256, 512, 0, 0, True, True, False, True),     # level-0 Conv_0: 2048 tiles, 4 per workgroup
+    (4, 128, 0, 128, 256, 512, 0, 0, True, False, True, True),     # level-0 Conv_1 + residual
+    (8, 128, 128, 128, 128, 256, 128, 128, True, False, False, True),  # up-path Conv_1 + cat shortcut (deferred GN)
+    (4, 128, 0, 128, 256, 512, 128, 0, True, False, True, True),   # Conv_1 + shortcut, 4 tiles per workgroup
+    (8, 256, 0, 256, 64, 128, 0, 0, True, True, False, True),      # two Cout tiles per image
+    (2, 256, 256, 256, 32, 64, 0, 0, False, False, True, False),   # cat input, no GN, fewer tiles than workgroups
+])
+def test_conv_halo6_persistent(gpu, case):
+    """Persistent halo GEMM (v6) vs an fp32 torch reference on the GPU at sizes where every
+    workgroup runs several tiles (the pipeline crosses chunk, tile and image boundaries),
+    with the fused GroupNorm+SiLU prologue, cat inputs, the 1x1 shortcut, temb, residual
+    and the per-channel output statistics."""
+    from snrse import ops
+    B, C0, C1, Co, H, W, Csc, Csc1, use_gn, use_temb, use_res, use_st = case
+    g = torch.Generator(device=gpu).manual_seed(sum(case[:8]))
+    Cin = C0 + C1
+    x0 = (torch.randn(B, H, W, C0, device=gpu, generator=g) * 1.3 + 0.1).bfloat16()
+    x1 = torch.randn(B, H, W, C1, device=gpu, generator=g).bfloat16() if C1 else None
+    xs0 = torch.randn(B, H, W, Csc, device=gpu, generator=g).bfloat16() if Csc else None
+    xs1 = torch.randn(B, H, W, Csc1, device=gpu, generator=g).bfloat16() if Csc1 else None
+    w = (torch.randn(Co, 3, 3, Cin, device=gpu, generator=g) / math.sqrt(9 * Cin)).bfloat16()
+    ws = (torch.randn(Co, Csc + Csc1, device=gpu, generator=g) / math.sqrt(Csc + Csc1 + 1)).bfloat16() if Csc else None
+    bias = torch.randn(Co, device=gpu, generator=g)
+    temb = torch.randn(B, Co + 40, device=gpu, generator=g) if use_temb else None
+    res = torch.randn(B, H, W, Co, device=gpu, generator=g).bfloat16() if use_res else None
+    xin = x0 if x1 is None else torch.cat([x0, x1], -1)
+    a = xin.float().permute(0, 3, 1, 2)
+    gn = None
+    if use_gn:
+        gam = torch.rand(Cin, device=gpu, generator=g) + 0.5
+        bet = torch.randn(Cin, device=gpu, generator=g) * 0.2
+        sums = ops.gn_stats(x0, x1)
+        gn = ops.gn_scale_shift(sums[0], gam, bet, H * W, sums1=sums[1])
+        a = F.silu(a * gn[0][:, :, None, None] + gn[1][:, :, None, None]).bfloat16().float()
+    ref = F.conv2d(a, w.float().permute(0, 3, 1, 2), bias, padding=1)
+    if Csc:
+        xs = xs0 if xs1 is None else torch.cat([xs0, xs1], -1)
+        ref = ref + torch.einsum("bhwc,oc->bohw", xs.float(), ws.float())
+    if use_temb:
+        ref = ref + temb[:, 40:40 + Co, None, None]
+    scale = 1 / math.sqrt(2) if use_res else 1.0
+    if use_res:
+        ref = ref + res.float().permute(0, 3, 1, 2)
+    ref = ref * scale
+    st = ops.new_stats(B, Co) if use_st else None
+    ops.set_option("conv_variant", 6)
+    try:
+        assert ops.conv_kernel_name() == "conv_halo6_kernel"
+        out = ops.conv2d(x0, w.reshape(Co, -1).contiguous(), 3, Co, bias=bias, src1=x1, sc=xs0, sc1=xs1, sc_wgt=ws,
+                         temb=temb, temb_off=40, res=res, out_scale=scale, stats=st, gn=gn)
+        torch.cuda.synchronize()
+    finally:
+        ops.set_option("conv_variant", 0)
+    got = out.float().permute(0, 3, 1, 2)
+    assert rel(got, ref) < 1e-2
+    if use_st:
+        o = out.double()
+        st_ref = torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)
+        assert rel(ops.fold_stats(st), st_ref) < 3e-3

@@ -17,7 +17,7 @@ from snrse import ops  # noqa: E402
 SHAPES = [
     (32, 128, 0, 128, 256, 512, 3, 0),
     (32, 128, 128, 128, 256, 512, 3, 0),   # up-path cat Conv_0
-    (32, 128, 0, 128, 256, 512, 3, 256),   # Conv_1 + 1x1 shortcut of a cat input
+    (32, 128, 0, 128, 256, 512, 3, 128),   # Conv_1 + 1x1 shortcut (Cin != Cout block)
     (32, 256, 0, 256, 128, 256, 3, 0),
     (32, 256, 0, 256, 64, 128, 3, 0),
     (32, 256, 256, 256, 32, 64, 3, 0),
@@ -25,7 +25,15 @@ SHAPES = [
 ]
 
 
-def run(shape, variant, reps, dev):
+def _gn_pair(B, C, dev, g):
+    """(scale, shift) views of one [2, B, C] tensor, the layout ops.gn_scale_shift returns."""
+    ss = torch.empty(2, B, C, device=dev)
+    ss[0] = torch.rand(B, C, device=dev, generator=g) + 0.5
+    ss[1] = torch.randn(B, C, device=dev, generator=g)
+    return ss[0], ss[1]
+
+
+def run(shape, variant, reps, dev, gn=False):
     B, C0, C1, Co, H, W, k, Csc = shape
     g = torch.Generator(device=dev).manual_seed(0)
     x0 = torch.randn(B, H, W, C0, device=dev, generator=g).bfloat16()
@@ -35,14 +43,17 @@ def run(shape, variant, reps, dev):
     ws = (torch.randn(Co, Csc, device=dev, generator=g) / 16).bfloat16() if Csc else None
     bias = torch.zeros(Co, device=dev)
     st = ops.new_stats(B, Co)
+    gnp = None
+    if gn and k == 3:
+        gnp = _gn_pair(B, C0 + C1, dev, g)
     ops.set_option("conv_variant", variant)
-    out = ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, stats=st)
+    out = ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, stats=st, gn=gnp)
     torch.cuda.synchronize()
     ts = []
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, out=out, stats=st)
+        ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, out=out, stats=st, gn=gnp)
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
@@ -54,9 +65,10 @@ def run(shape, variant, reps, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--variants", default="4,5,6")
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--shapes", default="", help="comma list of SHAPES indices (default all)")
+    ap.add_argument("--gn", action="store_true", help="fused GroupNorm+SiLU prologue (halo kernels)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     res = []
@@ -66,7 +78,7 @@ def main():
         row = {"shape": sh}
         for rnd in range(a.rounds):  # interleaved A/B rounds: clocks drift between launches
             for v in [int(x) for x in a.variants.split(",")]:
-                out, ms, fl = run(sh, v, a.reps, dev)
+                out, ms, fl = run(sh, v, a.reps, dev, gn=a.gn)
                 outs[v] = out.float()
                 ms = min(ms, row.get(f"v{v}_ms", ms))
                 row[f"v{v}_ms"] = ms

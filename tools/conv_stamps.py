@@ -21,10 +21,46 @@ sys.path.insert(0, PKG)
 STAMP_LIB = os.path.join(PKG, "lib", "stamps", "libsnrse_hip.so")
 
 
+def _gn_pair(B, C, dev, g):
+    """(scale, shift) views of one [2, B, C] tensor, the layout ops.gn_scale_shift returns."""
+    import torch
+    ss = torch.empty(2, B, C, device=dev)
+    ss[0] = torch.rand(B, C, device=dev, generator=g) + 0.5
+    ss[1] = torch.randn(B, C, device=dev, generator=g)
+    return ss[0], ss[1]
+
+
 def build():
     from snrse import build as b
     os.makedirs(os.path.dirname(STAMP_LIB), exist_ok=True)
     print(b.build_library(force=True, extra_flags=("-DSNRSE_STAMPS",), lib=STAMP_LIB))
+
+
+def v6_report(s, shape, ms):
+    """v6 stamps: 0 start, 1 prologue done, 2+2t / 3+2t epilogue start / end of local tile t
+    (t < 13), 28 loop end, 29 kernel end; 4 waves per workgroup."""
+    import numpy as np
+    s = s[:, :4]
+    s = s[s[:, 0, 29] != 0]
+    rel = s - s[:, :, :1]
+    out = {"shape": shape, "variant": 6, "ms": ms, "workgroups": int(s.shape[0]),
+           "wave_total_mean": float(rel[:, :, 29].mean()), "prologue": float(rel[:, :, 1].mean())}
+    mains, epis = [], []
+    prev = rel[:, :, 1]
+    for t in range(13):
+        st, en = rel[:, :, 2 + 2 * t], rel[:, :, 3 + 2 * t]
+        ok = en > 0
+        if not ok.any():
+            break
+        mains.append(float((st - prev)[ok].mean()))
+        epis.append(float((en - st)[ok].mean()))
+        prev = np.where(ok, en, prev)
+    out["tile_main"] = [round(x) for x in mains]
+    out["tile_epilogue"] = [round(x) for x in epis]
+    out["tail"] = float((rel[:, :, 29] - rel[:, :, 28]).mean())
+    cu = (s[:, 0, 31] << 16) | (s[:, 0, 30] & 0xFF00)
+    out["workgroups_per_cu"] = float(s.shape[0] / len(np.unique(cu)))
+    return out
 
 
 def main():
@@ -33,6 +69,7 @@ def main():
     ap.add_argument("--shapes", default="0")
     ap.add_argument("--variants", default="0")
     ap.add_argument("--stats", default="1", help="comma list of 0/1: fuse GN statistics")
+    ap.add_argument("--gn", action="store_true", help="fused GroupNorm+SiLU prologue")
     a = ap.parse_args()
     if a.build:
         return build()
@@ -55,25 +92,32 @@ def main():
         w = (torch.randn(Co, k * k * (C0 + C1), device=dev, generator=g) / 30).bfloat16()
         ws = (torch.randn(Co, Csc, device=dev, generator=g) / 16).bfloat16() if Csc else None
         bias = torch.zeros(Co, device=dev)
+        gnp = None
+        if a.gn:
+            gnp = _gn_pair(B, C0 + C1, dev, g)
         nblk = B * (H // 4) * (W // 64) * (Co // 128)
+        nblk = max(nblk, 1024)  # v6 is persistent: gridDim = min(tiles, 2 x CUs)
         buf = torch.zeros(nblk * 8 * 32, dtype=torch.int64, device=dev)
         for v, use_st in [(int(x), int(y)) for x in a.variants.split(",") for y in a.stats.split(",")]:
             ops.set_option("conv_variant", v)
             st = ops.new_stats(B, Co) if use_st else None
             lib.snrse_debug_set_stamps(None)
-            out = ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, stats=st)
+            out = ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, stats=st, gn=gnp)
             for _ in range(3):
-                ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, out=out, stats=st)
+                ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, out=out, stats=st, gn=gnp)
             buf.zero_()
             lib.snrse_debug_set_stamps(buf.data_ptr())
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, out=out, stats=st)
+            ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, out=out, stats=st, gn=gnp)
             e1.record()
             torch.cuda.synchronize()
             lib.snrse_debug_set_stamps(None)
             ms = e0.elapsed_time(e1)
             s = buf.view(nblk, 8, 32).cpu().numpy().astype(np.int64)
+            if v == 6:
+                print(json.dumps(v6_report(s, SHAPES[si], ms)), flush=True)
+                continue
             s = s[:, :4] if v == 5 else s  # v5 workgroups have 4 waves
             cin = C0 + C1
             kt = 32 if v == 5 else 64
