@@ -95,11 +95,11 @@ def conv_flops(src0, src1, ksize, cout, sc, sc1):
 
 
 class ConvProbe:
-    """HIP events on the launch stream around every launch of the dominant kernel — the halo
-    implicit-GEMM conv (bf16 3x3, Cout % 128 == 0, H % 4 == 0, W % 64 == 0, no Combine term; ops.halo_ok) —
-    during one extra enhance() pass after the timed region.  achieved = algorithmic FLOPs of
-    those launches / their summed event time, i.e. mean FLOPs per launch / mean launch
-    duration (the quantity rocprofv3 --stats reports as AverageNs for that kernel)."""
+    """HIP events on the launch stream around every halo-path conv launch (bf16 3x3, Cout % 128 == 0,
+    H % 4 == 0, W % 64 == 0; ops.halo_ok) during one extra enhance() pass after the timed region,
+    grouped by the kernel that ran (snrse_get_option "last_kernel").  achieved = algorithmic FLOPs of
+    the dominant kernel's launches / their summed event time, i.e. mean FLOPs per launch / mean
+    launch duration (the quantity rocprofv3 --stats reports as AverageNs for that kernel)."""
 
     def __init__(self):
         self.rec = []
@@ -109,13 +109,14 @@ class ConvProbe:
         probe = self
 
         def wrapped(src0, wgt, ksize, cout, *a, **kw):
-            if not ops.halo_ok(src0, ksize, cout) or kw.get("comb") is not None:
+            if not ops.halo_ok(src0, ksize, cout):
                 return orig(src0, wgt, ksize, cout, *a, **kw)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             out = orig(src0, wgt, ksize, cout, *a, **kw)
             e1.record()
-            probe.rec.append((conv_flops(src0, kw.get("src1"), ksize, cout, kw.get("sc"), kw.get("sc1")), e0, e1))
+            probe.rec.append((conv_flops(src0, kw.get("src1"), ksize, cout, kw.get("sc"), kw.get("sc1")), e0, e1,
+                              ops.kernel_name(ops.get_option("last_kernel"))))
             return out
 
         ops.conv2d = wrapped
@@ -125,10 +126,15 @@ class ConvProbe:
         self.ops.conv2d = self.orig
 
     def summary(self):
+        """{kernel: [flops, ms, launches]} over the probed pass."""
         torch.cuda.synchronize()
-        fl = sum(r[0] for r in self.rec)
-        ms = sum(r[1].elapsed_time(r[2]) for r in self.rec)
-        return fl, ms, len(self.rec)
+        by = {}
+        for fl, e0, e1, k in self.rec:
+            d = by.setdefault(k, [0.0, 0.0, 0])
+            d[0] += fl
+            d[1] += e0.elapsed_time(e1)
+            d[2] += 1
+        return by
 
 
 def pmc_traffic(kernel_prefix):
@@ -202,15 +208,18 @@ def main():
             enh(y, noise(999))
         finally:
             probe.uninstall()
-        fl, ms, n = probe.summary()
+        by = probe.summary()
+        kname = max(by, key=lambda k: by[k][1])  # the halo kernel with the most time in the step
+        fl, ms, n = by[kname]
         ach = fl / (ms * 1e-3) if ms > 0 else 0.0
         peak = PEAK[args.dtype]
-        kname = ops.conv_kernel_name()
         traffic, tsrc = pmc_traffic(kname)
         roof = {"bound": "mfma", "achieved": ach / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
                 "frac": ach / peak, "traffic": traffic, "kernel": kname, "launches_per_step": n,
                 "avg_launch_us": ms * 1e3 / max(n, 1), "flop_per_launch": fl / max(n, 1),
-                "kernel_ms_per_step": ms, "traffic_source": tsrc}
+                "kernel_ms_per_step": ms, "traffic_source": tsrc,
+                "other_halo_kernels": {k: {"launches": v[2], "ms": v[1], "tflops": v[0] / max(v[1], 1e-9) / 1e9}
+                                       for k, v in by.items() if k != kname}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -57,7 +57,8 @@ int snrse_upfirdn2d(const void* in, void* out, const float* kernel, int major, i
  *   gn_scale/gn_shift (optional, [B][C0+C1] f32, from snrse_gn_scale_shift): the main input
  *          is consumed as SiLU(x*scale+shift) (gn_act=1) or x*scale+shift (gn_act=0), i.e. the
  *          ResBlock's GroupNorm+SiLU fused into the GEMM's halo load (bf16, 3x3, H%4==0,
- *          W%64==0 only; otherwise hipErrorInvalidValue). */
+ *          W%64==0, and the pyramid heads Cout<=16 with f32 output; otherwise
+ *          hipErrorInvalidValue). */
 int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, int B, int H, int W, int ksize,
                  const void* wgt, const void* sc_src, int Csc, const void* sc_src1, int Csc1,
                  const void* sc_wgt, const float* bias, const float* temb, int temb_stride,
@@ -86,12 +87,34 @@ int snrse_gn_apply(const void* src0, int C0, const void* src1, int C1, int B, in
                    const double* sums, const double* sums1, const float* gamma, const float* beta,
                    int groups, float eps, int act, int mode, void* out, int dtype, hipStream_t stream);
 
+/* LDS-tiled GroupNorm-apply + SiLU + FIR x2 of a ResBlock with up/down (layerspp.py:245-257), bf16:
+ * out_act = FIR(act(x*scale+shift)) and, when out_raw != NULL, out_raw = FIR(x) (the shortcut input,
+ * layerspp.py:249/255), both [B][Ho][Wo][C] from one pass over x.  scale/shift [B][C] f32 from
+ * snrse_gn_scale_shift, or both NULL (identity).  mode 1 down (H, W even), 2 up.  C % 16 == 0. */
+int snrse_gn_resample(const void* src, int C, int B, int H, int W, const float* scale, const float* shift,
+                      int act, int mode, void* out_act, void* out_raw, hipStream_t stream);
+
+/* Elementwise GroupNorm-apply (+SiLU) of the channel concatenation (src0 | src1), bf16, from
+ * precomputed scale/shift [B][C0+C1] (both NULL: identity).  out [B][HW][C0+C1]. */
+int snrse_gn_act(const void* src0, int C0, const void* src1, int C1, int B, int HW, const float* scale,
+                 const float* shift, int act, void* out, hipStream_t stream);
+
+/* Split-K workspace of the small-image conv GEMMs (levels whose tile grid underfills the CUs): a
+ * device buffer of `bytes` the caller keeps alive and leaves untouched while convs run; the library
+ * keeps [splits][M][Cout] f32 partial sums there and splits only when they fit.  NULL disables
+ * splitting (the default).  One workspace per process: convs using it must share one stream. */
+int snrse_set_workspace(void* ptr, size_t bytes);
+
 /* Tuning switches (A/B experiments): "conv_variant" 0 auto, 1 register-staged v1, 2 LDS-DMA v2,
- * 4 halo kernel v4 with the register epilogue, 5 halo kernel v5 (two workgroups per CU). */
+ * 4 halo kernel v4 with the register epilogue, 5 halo kernel v5 (two workgroups per CU), 6
+ * persistent halo v6, 8 ping-pong halo v8 (6 / 8 fall back to 4 / 5 outside their contract);
+ * "splitk" 0 disables the split-K small-image GEMMs. */
 int snrse_set_option(const char* name, int value);
 
-/* Read back a switch: "conv_variant", or "halo_kernel" = generation of the halo conv kernel
- * the current setting dispatches to (4: conv_halo_kernel, 5: conv_halo5_kernel). */
+/* Read back a switch: "conv_variant", "splitk", "halo_kernel" = generation of the halo conv kernel
+ * the current setting dispatches to (4, 5, 6, 8), "last_kernel" = generation of the most recent
+ * snrse_conv2d launch (1 v1, 2 v2, 4/5/6/8 halo, 9 pyramid head), "last_ksplit" = K splits of the
+ * most recent v2 launch. */
 int snrse_get_option(const char* name, int* value);
 
 /* AttnBlockpp attention core (layerspp.py:84-88): qkv [B][L][3C] -> out [B][L][C],

@@ -515,8 +515,10 @@ __global__ __launch_bounds__(512) void conv_glds_kernel(ConvParams p) {
   const int nb = gridDim.x, bid = blockIdx.x;
   const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7, pos = bid >> 3;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
-  const int m0 = (wg / p.ntn) * BM;
-  const int n0 = (wg % p.ntn) * BN;
+  // split-K: the p.ksplit K ranges of one output tile are adjacent logical ids (same XCD)
+  const int ks = wg % p.ksplit, tl = wg / p.ksplit;
+  const int m0 = (tl / p.ntn) * BM;
+  const int n0 = (tl % p.ntn) * BN;
 
   const int HW = p.H * p.W;
   const int Cin = p.C0 + p.C1;
@@ -610,17 +612,19 @@ __global__ __launch_bounds__(512) void conv_glds_kernel(ConvParams p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  SNRSE_ISSUE(0, 0);
-  if (nk > 1) SNRSE_ISSUE(1, 1);
+  // this workgroup's K range (all of it unless split)
+  const int kb = (int)((long long)ks * nk / p.ksplit), ke = (int)((long long)(ks + 1) * nk / p.ksplit);
+  SNRSE_ISSUE(kb, 0);
+  if (ke - kb > 1) SNRSE_ISSUE(kb + 1, 1);
   const int lrow = lane & 15, lg = lane >> 4;
   int stage = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk)
+  for (int kt = kb; kt < ke; ++kt) {
+    if (kt + 1 < ke)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(AJ + BJ) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + 2 < nk) SNRSE_ISSUE(kt + 2, stage == 0 ? 2 : stage - 1);
+    if (kt + 2 < ke) SNRSE_ISSUE(kt + 2, stage == 0 ? 2 : stage - 1);
     const char* sa = smem + stage * STAGE;
     const char* sb = sa + A_BYTES;
 #pragma unroll
@@ -638,11 +642,122 @@ __global__ __launch_bounds__(512) void conv_glds_kernel(ConvParams p) {
     stage = stage == STAGES - 1 ? 0 : stage + 1;
   }
 #undef SNRSE_ISSUE
+  if (p.ksplit > 1) {  // raw fp32 partial sums of this K range; conv_splitk_finalize applies the epilogue
+    float* const wsp = p.ws + (size_t)ks * p.M * p.Cout;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm * TM + i * 16 + lg * 4 + e;
+        if (m < p.M) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) wsp[(size_t)m * p.Cout + n0 + wn * TN + j * 16 + lrow] = acc[i][j][e];
+        }
+      }
+    return;
+  }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   const int b_lo = m0 / HW, b_hi = (min(m0 + BM, p.M) - 1) / HW;
   epilogue_lds<TO, WM, BN>(p, acc, m0 + wm * TM, n0 + wn * TN, lane, (float*)(smem + wid * (64 * 68 * 4)),
                            (float*)(smem + 8 * (64 * 68 * 4)), wm, b_lo == b_hi ? b_lo : -1, n0);
+}
+
+// Split-K finalize of the v2 GEMM: out = epilogue(sum of the p.ksplit partial-sum planes in p.ws).
+// Block = 16 pixel rows x 16 lanes of 8 channels (128 channels) walking `ppb` pixels of one image,
+// so the GroupNorm statistics leave as one atomic pair per channel per block.
+template <typename TO>
+__global__ __launch_bounds__(256) void conv_splitk_finalize(ConvParams p, int ppb) {
+  __shared__ float red[16 * 256];
+  const int HW = p.H * p.W;
+  const int nbi = (HW + ppb - 1) / ppb;
+  const int b = blockIdx.x / nbi;
+  const int px0 = (blockIdx.x - b * nbi) * ppb, px1 = min(HW, px0 + ppb);
+  const int cl = (threadIdx.x & 15) * 8, r0 = threadIdx.x >> 4;
+  const int n = blockIdx.y * 128 + cl;
+  float add[8], cw[8][4], cb[8], s1[8], s2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    add[k] = (p.bias ? p.bias[n + k] : 0.f) + (p.temb ? p.temb[(size_t)b * p.temb_stride + n + k] : 0.f);
+    s1[k] = 0.f;
+    s2[k] = 0.f;
+    cb[k] = 0.f;
+    cw[k][0] = cw[k][1] = cw[k][2] = cw[k][3] = 0.f;
+    if (p.comb_src) {
+      cw[k][0] = p.comb_w[(n + k) * 4 + 0];
+      cw[k][1] = p.comb_w[(n + k) * 4 + 1];
+      cw[k][2] = p.comb_w[(n + k) * 4 + 2];
+      cw[k][3] = p.comb_w[(n + k) * 4 + 3];
+      cb[k] = p.comb_b[n + k];
+    }
+  }
+  const size_t plane = (size_t)p.M * p.Cout;
+  for (int px = px0 + r0; px < px1; px += 16) {
+    const size_t m = (size_t)b * HW + px;
+    const float* w = p.ws + m * p.Cout + n;
+    f32x4 a0 = *(const f32x4*)w, a1 = *(const f32x4*)(w + 4);
+    for (int s = 1; s < p.ksplit; ++s) {
+      a0 += *(const f32x4*)(w + s * plane);
+      a1 += *(const f32x4*)(w + s * plane + 4);
+    }
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k] = a0[k] + add[k];
+      v[4 + k] = a1[k] + add[4 + k];
+    }
+    if (p.res) {
+      if constexpr (sizeof(TO) == 2) {
+        const u32x4 rv = *(const u32x4*)((const bf16_t*)p.res + m * p.res_ld + n);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] += __uint_as_float(rv[k] << 16);
+          v[2 * k + 1] += __uint_as_float(rv[k] & 0xffff0000u);
+        }
+      } else {
+        const float* rp = (const float*)p.res + m * p.res_ld + n;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] += rp[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] *= p.out_scale;
+    if (p.comb_src) {
+      const f32x4 q = *(const f32x4*)(p.comb_src + m * 4);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += q[0] * cw[k][0] + q[1] * cw[k][1] + q[2] * cw[k][2] + q[3] * cw[k][3] + cb[k];
+    }
+    if constexpr (sizeof(TO) == 2) {
+      u32x4 o;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = pack_bf16x2(v[2 * k], v[2 * k + 1]);
+      *(u32x4*)((bf16_t*)p.out + m * p.out_ld + n) = o;
+    } else {
+      float* op = (float*)p.out + m * p.out_ld + n;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) op[k] = v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s1[k] += v[k];
+      s2[k] = fmaf(v[k], v[k], s2[k]);
+    }
+  }
+  if (p.stats) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[r0 * 256 + (cl + k) * 2] = s1[k];
+      red[r0 * 256 + (cl + k) * 2 + 1] = s2[k];
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    float a = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a += red[r * 256 + t];
+    unsafeAtomicAdd(&p.stats[stat_idx(b, blockIdx.x & (SNRSE_STAT_SLOTS - 1), blockIdx.y * 128 + (t >> 1), p.Cout) +
+                             (t & 1)],
+                    (double)a);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1146,6 +1261,23 @@ int launch_conv(ConvParams p, int npad, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+float* g_ws = nullptr;   // split-K workspace (snrse_set_workspace)
+size_t g_ws_bytes = 0;
+int g_splitk = 1;        // option "splitk": 0 disables K splitting
+int g_last_ksplit = 1;   // option read-back "last_ksplit": splits of the latest v2 launch
+
+// K splits for a v2 launch of `tiles` output tiles over nk K-tiles: about one workgroup per CU when
+// the tile grid alone underfills the chip (the small NCSN++ levels), >= 4 K-tiles per split, and
+// the partial sums within the registered workspace
+int choose_ksplit(const ConvParams& p, int tiles, int nk) {
+  if (!g_splitk || !g_ws || tiles >= 192) return 1;
+  int s = (256 + tiles - 1) / tiles;
+  if (s > nk / 4) s = nk / 4;
+  const size_t plane = (size_t)p.M * p.Cout * sizeof(float);
+  if ((size_t)s * plane > g_ws_bytes) s = (int)(g_ws_bytes / plane);
+  return s >= 2 ? s : 1;
+}
+
 template <int BM, int BN, typename TO>
 int launch_glds(ConvParams p, hipStream_t s) {
   constexpr size_t lds = (size_t)3 * (BM + BN) * 128;
@@ -1157,15 +1289,29 @@ int launch_glds(ConvParams p, hipStream_t s) {
   }
   p.ntn = p.Cout / BN;
   const int ntm = (p.M + BM - 1) / BM;
-  hipLaunchKernelGGL((conv_glds_kernel<BM, BN, TO>), dim3(ntm * p.ntn), dim3(512), lds, s, p);
+  const int nk = p.ksize * p.ksize * ((p.C0 + p.C1) / 64) + (p.sc_src ? (p.Csc + p.Csc1) / 64 : 0);
+  p.ksplit = choose_ksplit(p, ntm * p.ntn, nk);
+  p.ws = g_ws;
+  g_last_ksplit = p.ksplit;
+  hipLaunchKernelGGL((conv_glds_kernel<BM, BN, TO>), dim3(ntm * p.ntn * p.ksplit), dim3(512), lds, s, p);
+  if (p.ksplit > 1) {
+    SNRSE_LAUNCH_CHECK();
+    const int HW = p.H * p.W, ppb = 64;
+    hipLaunchKernelGGL((conv_splitk_finalize<TO>), dim3(p.B * ((HW + ppb - 1) / ppb), p.Cout / 128), dim3(256), 0, s,
+                       p, ppb);
+  }
   return (int)hipGetLastError();
 }
 
-int g_conv_variant = 0;  // 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 4 halo w/ scalar epilogue, 5 halo v5, 6 persistent halo v6 (falls back to v4 outside its contract)
+// 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 4 halo w/ scalar epilogue, 5 halo v5,
+// 6 persistent halo v6, 8 ping-pong halo v8 (v6 / v8 fall back to v4 / v5 outside their contract)
+int g_conv_variant = 0;
 constexpr int kHaloAuto = 5;  // halo kernel generation taken by variant 0 (fastest measured: profiles/)
+int g_last_kernel = 0;        // option read-back "last_kernel": generation of the latest launch (9 = head)
 
 template <typename T, typename TO>
 int dispatch_conv(const ConvParams& p, hipStream_t s) {
+  const int hk = g_conv_variant == 0 ? kHaloAuto : g_conv_variant;
   if (p.Cout >= 64) {
     if (p.Cout % 128 != 0) return SNRSE_EINVAL;
     if constexpr (sizeof(T) == 2) {
@@ -1174,22 +1320,41 @@ int dispatch_conv(const ConvParams& p, hipStream_t s) {
       if (g_conv_variant != 1 && fits) {
         if (g_conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0) {
           if constexpr (sizeof(TO) == 2) {
-            if ((g_conv_variant == 6 || (g_conv_variant == 0 && kHaloAuto == 6)) && halo6_ok(p))
+            if (hk == 8 && halo8_ok(p)) {
+              g_last_kernel = 8;
+              return launch_halo8(p, s);
+            }
+            if (hk == 6 && halo6_ok(p)) {
+              g_last_kernel = 6;
               return launch_halo6(p, s);
+            }
           }
-          if (g_conv_variant == 5 || (g_conv_variant == 0 && kHaloAuto == 5)) return launch_halo5<TO>(p, s);
+          if (hk == 5 || hk == 8) {
+            g_last_kernel = 5;
+            return launch_halo5<TO>(p, s);
+          }
+          g_last_kernel = 4;
           return g_conv_variant == 4 ? launch_halo<TO, false>(p, s) : launch_halo<TO, true>(p, s);
         }
-        if (p.gn_scale) return SNRSE_EINVAL;  // fused GroupNorm exists only on the halo path
+        if (p.gn_scale) return SNRSE_EINVAL;  // fused GroupNorm exists only on the halo paths
+        g_last_kernel = 2;
         if (p.Cout % 256 == 0) return launch_glds<128, 256, TO>(p, s);
         return launch_glds<256, 128, TO>(p, s);
       }
     }
     if (p.gn_scale) return SNRSE_EINVAL;
+    g_last_kernel = 1;
     return launch_conv<T, TO, 128, 128, 2, 2>(p, p.Cout, s);
+  }
+  if constexpr (sizeof(T) == 2 && sizeof(TO) == 4) {
+    if (g_conv_variant != 1 && head_ok(p)) {
+      g_last_kernel = 9;
+      return launch_head(p, s);
+    }
   }
   if (p.gn_scale) return SNRSE_EINVAL;
   if (p.Cout > 16) return SNRSE_EINVAL;
+  g_last_kernel = 1;
   return launch_conv<T, TO, 128, 16, 4, 1>(p, 16, s);
 }
 
@@ -1225,6 +1390,7 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
   p.comb_src = comb_src; p.comb_w = comb_w; p.comb_b = comb_b;
   p.out = out; p.Cout = Cout; p.out_ld = out_ld; p.M = B * H * W;
   p.stats = stats;
+  p.ws = nullptr; p.ksplit = 1;
   p.gn_scale = gn_scale; p.gn_shift = gn_shift; p.gn_act = gn_act;
   if ((gn_scale == nullptr) != (gn_shift == nullptr)) return SNRSE_EINVAL;
   if (p.M <= 0) return 0;
@@ -1262,20 +1428,25 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   if (name_is(name, "conv_variant")) { *value = g_conv_variant; return 0; }
   if (name_is(name, "halo_kernel")) {  // generation taken by a halo-eligible bf16 conv
     const int v = g_conv_variant == 0 ? kHaloAuto : g_conv_variant;
-    *value = (v == 6 || v == 5) ? v : 4;
+    *value = (v == 8 || v == 6 || v == 5) ? v : 4;
     return 0;
   }
+  if (name_is(name, "last_kernel")) { *value = g_last_kernel; return 0; }
+  if (name_is(name, "splitk")) { *value = g_splitk; return 0; }
+  if (name_is(name, "last_ksplit")) { *value = g_last_ksplit; return 0; }
   return SNRSE_EINVAL;
 }
 
 extern "C" int snrse_set_option(const char* name, int value) {
   if (!name) return SNRSE_EINVAL;
-  const char* k = "conv_variant";
-  int i = 0;
-  while (k[i] && name[i] == k[i]) ++i;
-  if (k[i] == 0 && name[i] == 0) {
-    g_conv_variant = value;
-    return 0;
-  }
+  if (name_is(name, "conv_variant")) { g_conv_variant = value; return 0; }
+  if (name_is(name, "splitk")) { g_splitk = value; return 0; }
   return SNRSE_EINVAL;
+}
+
+extern "C" int snrse_set_workspace(void* ptr, size_t bytes) {
+  if (!ptr && bytes) return SNRSE_EINVAL;
+  g_ws = (float*)ptr;
+  g_ws_bytes = ptr ? bytes : 0;
+  return 0;
 }

@@ -39,6 +39,8 @@ struct ConvParams {
   const float* gn_scale;  // optional [B][Cin] GroupNorm scale/shift applied to the main input (halo path)
   const float* gn_shift;
   int gn_act;             // SiLU after the GroupNorm affine
+  float* ws;              // split-K partial sums [ksplit][M][Cout] f32 (caller-registered workspace)
+  int ksplit;             // K splits of the v2 GEMM (1: the epilogue runs in the GEMM itself)
   unsigned long long* stamps;  // timing-diagnostic build only (-DSNRSE_STAMPS): [blocks][8][32]
 };
 
@@ -91,5 +93,11 @@ SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
 // SNRSE_EINVAL when the shape / operands are outside its contract.
 int launch_halo6(const ConvParams& p, hipStream_t s);
 bool halo6_ok(const ConvParams& p);
+// 8-wave ping-pong halo GEMM (conv_halo8.hip): ResBlock convs without shortcut / Combine, H % 8 == 0.
+int launch_halo8(const ConvParams& p, hipStream_t s);
+bool halo8_ok(const ConvParams& p);
+// Pyramid heads (conv_head.hip): 3x3, Cout <= 16, f32 output, optional fused GroupNorm+SiLU.
+int launch_head(const ConvParams& p, hipStream_t s);
+bool head_ok(const ConvParams& p);
 
 }  // namespace snrse_conv

@@ -1,0 +1,168 @@
+// Pyramid-head 3x3 convolution (Cout <= 16, f32 output) with the fused GroupNorm+SiLU prologue:
+// the NCSNpp output_skip heads  pyr = conv3x3(SiLU(GN(h)), C -> 4) + up2(pyr)  (ncsnpp.py:348-366,
+// layers.py:100-110).  The generic register-staged GEMM (conv_mfma_kernel) re-read every input pixel
+// nine times through an im2col tile and synchronised per 64-channel k-step for 4 useful output
+// channels; here the (4+2) x (64+2) halo of each 32-channel chunk is staged once (GroupNorm+SiLU
+// applied in registers, zero padding kept), all 9 taps read it from LDS, and the next chunk's halo
+// is loaded into registers under the current chunk's MFMAs.  The kernel is bound by one HBM pass
+// over h; each wave owns one image row of 64 px x 16 channels (4 of them real).
+#include "conv_common.h"
+
+namespace snrse_conv {
+namespace {
+
+constexpr int KH_TH = 4, KH_TW = 64, KH_HC = KH_TW + 2;
+constexpr int KH_HROWS = (KH_TH + 2) * KH_HC;  // 396
+constexpr int KH_HJ = 7;                       // halo rows per thread: (tid >> 2) + 64 j
+constexpr int KH_HALO = KH_HROWS * 64;         // 25344 B
+constexpr int KH_WP = 9 * 16 * 4;              // 16-B weight pieces of one chunk: 9 taps x 16 co x 4
+constexpr int KH_WJ = (KH_WP + 255) / 256;     // per thread (3)
+constexpr int KH_LDS = KH_HALO + 9 * 1024;     // + 9 taps x 16 co x 64 B = 34560 B
+
+SNRSE_DEV int kh_swz(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >> 1) & 3)) << 4); }
+
+#define KH_LOAD(C_)                                                                                            \
+  do {                                                                                                         \
+    const int ch_ = (C_) * 32;                                                                                 \
+    const bool u1_ = ch_ >= p.C0;                                                                              \
+    const __amdgpu_buffer_rsrc_t r_ = u1_ ? make_rsrc(p.src1, p.bytes1) : make_rsrc(p.src0, p.bytes0);         \
+    const int cs_ = u1_ ? p.C1 : p.C0, cc_ = (u1_ ? ch_ - p.C0 : ch_) + hcol * 8;                              \
+    _Pragma("unroll") for (int j = 0; j < KH_HJ; ++j) {                                                        \
+      const int voff_ = hok[j] ? (hpix[j] * cs_ + cc_) * 2 : (int)0x80000000;                                  \
+      hv[j] = __builtin_amdgcn_raw_buffer_load_b128(r_, voff_, 0, 0);                                          \
+    }                                                                                                          \
+    _Pragma("unroll") for (int k = 0; k < KH_WJ; ++k) {                                                        \
+      const int pc_ = tid + 256 * k; /* tap (pc >> 6), co ((pc >> 2) & 15), 16-B chunk (pc & 3) */              \
+      const int voff_ = pc_ < KH_WP ? ((((pc_ >> 2) & 15) * K1 + (pc_ >> 6) * Cin + ch_ + (pc_ & 3) * 8) * 2)   \
+                                    : (int)0x80000000;                                                         \
+      wv[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, voff_, 0, 0);                                          \
+    }                                                                                                          \
+    if (gn) {                                                                                                  \
+      const float* sp_ = p.gn_scale + (size_t)b * Cin + ch_ + hcol * 8;                                        \
+      const float* hp_ = p.gn_shift + (size_t)b * Cin + ch_ + hcol * 8;                                        \
+      gs0 = *(const f32x4*)sp_;                                                                                \
+      gs1 = *(const f32x4*)(sp_ + 4);                                                                          \
+      gh0 = *(const f32x4*)hp_;                                                                                \
+      gh1 = *(const f32x4*)(hp_ + 4);                                                                          \
+    }                                                                                                          \
+  } while (0)
+
+// grid: B * (H / 4) * (W / 64) workgroups of 256
+__global__ __launch_bounds__(256) void conv_head_kernel(ConvParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[KH_LDS];
+  char* const halo = smem;
+  char* const wsl = smem + KH_HALO;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntw = p.W / KH_TW, nth = p.H / KH_TH;
+  int t = blockIdx.x;
+  const int w0 = (t % ntw) * KH_TW;
+  t /= ntw;
+  const int h0 = (t % nth) * KH_TH;
+  const int b = t / nth;
+  const int Cin = p.C0 + p.C1;
+  const int nc = Cin >> 5;
+  const int K1 = 9 * Cin;
+  const int hcol = tid & 3;
+  const bool gn = p.gn_scale != nullptr;
+  const int lrow = lane & 15, lg = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.wgt, p.wbytes);
+
+  int hpix[KH_HJ];
+  bool hok[KH_HJ];
+#pragma unroll
+  for (int j = 0; j < KH_HJ; ++j) {
+    const int hr = (tid >> 2) + 64 * j;
+    const int hy = hr / KH_HC, hx = hr - hy * KH_HC;
+    const int ih = h0 + hy - 1, iw = w0 + hx - 1;
+    hok[j] = hr < KH_HROWS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+    hpix[j] = (b * p.H + ih) * p.W + iw;
+  }
+  u32x4 hv[KH_HJ], wv[KH_WJ];
+  f32x4 gs0 = {1.f, 1.f, 1.f, 1.f}, gs1 = gs0, gh0 = {0.f, 0.f, 0.f, 0.f}, gh1 = gh0;
+
+  // acc[i]: D[co = 4 lg + e][px = w0 + 16 i + lrow]  (A = weights, B = halo pixels)
+  f32x4 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  KH_LOAD(0);
+  for (int c = 0; c < nc; ++c) {
+    // registers -> LDS: GroupNorm + SiLU on the halo (rows outside the image stay zero), weights
+#pragma unroll
+    for (int j = 0; j < KH_HJ; ++j) {
+      const int hr = (tid >> 2) + 64 * j;
+      if (j == KH_HJ - 1 && hr >= KH_HROWS) break;
+      u32x4 v = hv[j];
+      if (gn) {
+        const float sc[8] = {gs0[0], gs0[1], gs0[2], gs0[3], gs1[0], gs1[1], gs1[2], gs1[3]};
+        const float sh[8] = {gh0[0], gh0[1], gh0[2], gh0[3], gh1[0], gh1[1], gh1[2], gh1[3]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float lo = fmaf(__uint_as_float(v[i] << 16), sc[2 * i], sh[2 * i]);
+          float hi = fmaf(__uint_as_float(v[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]);
+          if (p.gn_act) {
+            lo = silu(lo);
+            hi = silu(hi);
+          }
+          v[i] = hok[j] ? pack_bf16x2(lo, hi) : 0u;
+        }
+      }
+      *(u32x4*)(halo + kh_swz(hr, hcol)) = v;
+    }
+#pragma unroll
+    for (int k = 0; k < KH_WJ; ++k) {
+      const int pc = tid + 256 * k;
+      if (pc < KH_WP) *(u32x4*)(wsl + (pc >> 6) * 1024 + kh_swz((pc >> 2) & 15, pc & 3)) = wv[k];
+    }
+    __syncthreads();
+    if (c + 1 < nc) KH_LOAD(c + 1);
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) {
+      const int dy = tp / 3 - 1, dx = tp % 3 - 1;
+      const int hbase = (wid + dy + 1) * KH_HC + dx + 1 + lrow;
+      const u32x4 a = *(const u32x4*)(wsl + tp * 1024 + kh_swz(lrow, lg));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const u32x4 bx = *(const u32x4*)(halo + kh_swz(hbase + 16 * i, lg));
+        acc[i] = mfma_chunk<bf16_t>(a, bx, acc[i]);
+      }
+    }
+    __syncthreads();
+  }
+  // epilogue: lanes with 4 lg < Cout hold channels 4 lg .. 4 lg + 3 of one pixel
+  const int co = 4 * lg;
+  if (co < p.Cout) {
+    f32x4 add = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias) add = f32x4{p.bias[co], p.bias[co + 1], p.bias[co + 2], p.bias[co + 3]};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const size_t m = ((size_t)b * p.H + h0 + wid) * p.W + w0 + 16 * i + lrow;
+      f32x4 v = acc[i] + add;
+      if (p.res) v += *(const f32x4*)((const float*)p.res + m * p.res_ld + co);
+      v *= p.out_scale;
+      *(f32x4*)((float*)p.out + m * p.out_ld + co) = v;
+    }
+  }
+}
+#undef KH_LOAD
+
+}  // namespace
+
+bool head_ok(const ConvParams& p) {
+  if (p.ksize != 3 || p.Cout > 16 || p.Cout % 4 || p.H % KH_TH || p.W % KH_TW || p.B <= 0) return false;
+  if (p.C0 % 32 || p.C1 % 32 || p.C0 + p.C1 <= 0) return false;
+  if (p.sc_src || p.temb || p.comb_src || p.stats) return false;
+  if (p.out_ld % 4 || (p.res && p.res_ld % 4)) return false;
+  const long long lim = 0x7ff00000ll;
+  return p.bytes0 < lim && p.bytes1 < lim && p.wbytes < lim;
+}
+
+int launch_head(const ConvParams& p, hipStream_t s) {
+  if (!head_ok(p)) return SNRSE_EINVAL;
+  const long long tiles = (long long)p.B * (p.H / KH_TH) * (p.W / KH_TW);
+  if (tiles <= 0 || tiles > 0x7fffffffLL) return SNRSE_EINVAL;
+  hipLaunchKernelGGL(conv_head_kernel, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  return (int)hipGetLastError();
+}
+
+}  // namespace snrse_conv

@@ -1,0 +1,239 @@
+// LDS-tiled GroupNorm-apply + SiLU + FIR [1,3,3,1] down/up-sampling, and the elementwise
+// GroupNorm-apply (+ SiLU) over a channel concatenation, both from precomputed per-(b, c)
+// scale / shift (snrse_gn_scale_shift).  bf16 storage, f32 arithmetic (gfx950).
+//
+// Reference ops replaced (BigGAN ResBlock with up / down, layerspp.py:245-268):
+//   h = act(GroupNorm_0(x)); h = upsample_2d / downsample_2d(h, fir_kernel)   (:245-257)
+//   x = upsample_2d / downsample_2d(x, fir_kernel)  -- the shortcut input     (:249, :255)
+//   up_or_down_sampling.py:195-257 (upfirdn2d with k = outer([1,3,3,1]) / 64, gain 1 (down)
+//   or 4 (up), zero padding of the activated tensor).
+// One pass reads x once, activates every input pixel once (the per-output gn_apply kernel
+// re-activated each input 4x (down) / 16x (up) and folded the statistics in every block), and
+// writes both the activated and the raw resampled tensors; the block's input tile is staged in
+// LDS as f32 (activated) + bf16 (raw).
+#include "common.h"
+
+namespace {
+
+constexpr int kCB = 16;  // channels per block (two 8 x bf16 vectors per pixel)
+constexpr int kNV = kCB / 8;
+
+enum { MODE_DOWN = 1, MODE_UP = 2 };
+
+template <int MODE> struct RTile;
+// down x2: out[i] = sum_a k[a] x[2i + a - 1]; out tile 8 x 16 <- in tile 18 x 34
+template <> struct RTile<MODE_DOWN> {
+  static constexpr int OTY = 8, OTX = 16, ITY = 2 * OTY + 2, ITX = 2 * OTX + 2;
+  SNRSE_DEV static int in0(int o0) { return 2 * o0 - 1; }
+};
+// up x2: out[2q] = (x[q-1] + 3 x[q]) / 4, out[2q+1] = (3 x[q] + x[q+1]) / 4; out tile 16 x 32 <- in 10 x 18
+template <> struct RTile<MODE_UP> {
+  static constexpr int OTY = 16, OTX = 32, ITY = OTY / 2 + 2, ITX = OTX / 2 + 2;
+  SNRSE_DEV static int in0(int o0) { return o0 / 2 - 1; }
+};
+
+SNRSE_DEV void unpack8(const u32x4 r, float* v) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(r[i] << 16);
+    v[2 * i + 1] = __uint_as_float(r[i] & 0xffff0000u);
+  }
+}
+
+SNRSE_DEV u32x4 pack8(const float* v) {
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
+  return r;
+}
+
+// Linear block id -> XCD-contiguous logical id: consecutive workgroups are dealt round-robin over
+// the 8 XCDs, so without the remap the channel groups of one pixel tile (which share every
+// 128-byte line of the input) would be fetched by 8 different L2s.
+SNRSE_DEV int xcd_logical(int i, int n) {
+  if (n & 7) return i;
+  return (i & 7) * (n >> 3) + (i >> 3);
+}
+
+// grid: B * tiles_y * tiles_x * (C / 16) blocks of 256.  scale/shift [B][C] f32 or null (identity).
+template <int MODE>
+__global__ __launch_bounds__(256) void gn_resample_kernel(const bf16_t* __restrict__ src, int C, int H, int W,
+                                                          int tiles_x, int tiles_y, const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, int act,
+                                                          bf16_t* __restrict__ out_act, bf16_t* __restrict__ out_raw) {
+  using T = RTile<MODE>;
+  constexpr int NPX = T::ITY * T::ITX;
+  __shared__ __attribute__((aligned(16))) float s_act[NPX * kCB];
+  __shared__ __attribute__((aligned(16))) bf16_t s_raw[NPX * kCB];
+  const int ncg = C / kCB;
+  int id = xcd_logical(blockIdx.x, gridDim.x);
+  const int cg = id % ncg;
+  id /= ncg;
+  const int tx = id % tiles_x;
+  id /= tiles_x;
+  const int ty = id % tiles_y;
+  const int b = id / tiles_y;
+  const int Ho = MODE == MODE_DOWN ? H / 2 : 2 * H, Wo = MODE == MODE_DOWN ? W / 2 : 2 * W;
+  const int oy0 = ty * T::OTY, ox0 = tx * T::OTX;
+  const int iy0 = T::in0(oy0), ix0 = T::in0(ox0);
+  const int c0 = cg * kCB;
+  const int tid = threadIdx.x;
+
+  // stage: raw bf16 + act(x * scale + shift) f32; outside the image both are zero (zero padding)
+  for (int idx = tid; idx < NPX * kNV; idx += 256) {
+    const int v = idx % kNV, p = idx / kNV;
+    const int ly = p / T::ITX, lx = p - ly * T::ITX;
+    const int iy = iy0 + ly, ix = ix0 + lx;
+    u32x4 r = {0u, 0u, 0u, 0u};
+    float a[8];
+    const int c = c0 + 8 * v;
+    if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
+      r = *(const u32x4*)(src + (((size_t)b * H + iy) * W + ix) * C + c);
+      float x[8];
+      unpack8(r, x);
+      if (scale) {
+        const float* sp = scale + (size_t)b * C + c;
+        const float* hp = shift + (size_t)b * C + c;
+        const f32x4 s0 = *(const f32x4*)sp, s1 = *(const f32x4*)(sp + 4);
+        const f32x4 h0 = *(const f32x4*)hp, h1 = *(const f32x4*)(hp + 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          x[i] = fmaf(x[i], s0[i], h0[i]);
+          x[i + 4] = fmaf(x[i + 4], s1[i], h1[i]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = act ? silu(x[i]) : x[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a[i] = 0.f;
+    }
+    *(u32x4*)(s_raw + p * kCB + 8 * v) = r;
+    f32x4* d = (f32x4*)(s_act + p * kCB + 8 * v);
+    d[0] = f32x4{a[0], a[1], a[2], a[3]};
+    d[1] = f32x4{a[4], a[5], a[6], a[7]};
+  }
+  __syncthreads();
+
+  constexpr int NOUT = T::OTY * T::OTX * kNV;
+  for (int idx = tid; idx < NOUT; idx += 256) {
+    const int v = idx % kNV, p = idx / kNV;
+    const int ly = p / T::OTX, lx = p - ly * T::OTX;
+    const int oy = oy0 + ly, ox = ox0 + lx;
+    if (oy >= Ho || ox >= Wo) continue;
+    float oa[8], orw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      oa[i] = 0.f;
+      orw[i] = 0.f;
+    }
+    auto tap = [&](int py, int px, float w) {
+      const int q = (py * T::ITX + px) * kCB + 8 * v;
+      const f32x4 a0 = *(const f32x4*)(s_act + q), a1 = *(const f32x4*)(s_act + q + 4);
+      float x[8];
+      unpack8(*(const u32x4*)(s_raw + q), x);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        oa[i] = fmaf(a0[i], w, oa[i]);
+        oa[i + 4] = fmaf(a1[i], w, oa[i + 4]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) orw[i] = fmaf(x[i], w, orw[i]);
+    };
+    if constexpr (MODE == MODE_DOWN) {
+      const float k1[4] = {0.125f, 0.375f, 0.375f, 0.125f};
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) tap(2 * ly + a, 2 * lx + bb, k1[a] * k1[bb]);
+    } else {
+      // tile origins are even, so the local parity is the global one
+      const int y0 = ((ly & 1) ? (ly >> 1) : (ly >> 1) - 1) + 1, x0 = ((lx & 1) ? (lx >> 1) : (lx >> 1) - 1) + 1;
+      const float wy0 = (ly & 1) ? 0.75f : 0.25f, wx0 = (lx & 1) ? 0.75f : 0.25f;
+      tap(y0, x0, wy0 * wx0);
+      tap(y0, x0 + 1, wy0 * (1.f - wx0));
+      tap(y0 + 1, x0, (1.f - wy0) * wx0);
+      tap(y0 + 1, x0 + 1, (1.f - wy0) * (1.f - wx0));
+    }
+    const size_t o = (((size_t)b * Ho + oy) * Wo + ox) * C + c0 + 8 * v;
+    *(u32x4*)(out_act + o) = pack8(oa);
+    if (out_raw) *(u32x4*)(out_raw + o) = pack8(orw);
+  }
+}
+
+// out [B][HW][C0 + C1] = act(x * scale + shift) of the channel concatenation (src0 | src1).
+// grid (nblk, B): each block stages its image's scale / shift in LDS.
+__global__ __launch_bounds__(256) void gn_act_kernel(const bf16_t* __restrict__ src0, int C0,
+                                                     const bf16_t* __restrict__ src1, int C1, int HW,
+                                                     int pix_per_blk, const float* __restrict__ scale,
+                                                     const float* __restrict__ shift, int act,
+                                                     bf16_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float s_ss[];  // scale[C], shift[C]
+  const int C = C0 + C1;
+  const int b = blockIdx.y;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    s_ss[c] = scale ? scale[(size_t)b * C + c] : 1.f;
+    s_ss[C + c] = scale ? shift[(size_t)b * C + c] : 0.f;
+  }
+  __syncthreads();
+  const int LP = C / 8;
+  const int p0 = blockIdx.x * pix_per_blk;
+  const int p1 = min(HW, p0 + pix_per_blk);
+  const int total = (p1 - p0) * LP;
+  for (int idx = threadIdx.x; idx < total; idx += 256) {
+    const int pix = p0 + idx / LP;
+    const int c = (idx % LP) * 8;
+    const bf16_t* s = c < C0 ? src0 + ((size_t)b * HW + pix) * C0 + c : src1 + ((size_t)b * HW + pix) * C1 + (c - C0);
+    float x[8];
+    unpack8(*(const u32x4*)s, x);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float y = fmaf(x[i], s_ss[c + i], s_ss[C + c + i]);
+      x[i] = act ? silu(y) : y;
+    }
+    *(u32x4*)(out + ((size_t)b * HW + pix) * C + c) = pack8(x);
+  }
+}
+
+template <int MODE>
+int launch_resample(const void* src, int C, int B, int H, int W, const float* scale, const float* shift, int act,
+                    void* out_act, void* out_raw, hipStream_t stream) {
+  using T = RTile<MODE>;
+  const int Ho = MODE == MODE_DOWN ? H / 2 : 2 * H, Wo = MODE == MODE_DOWN ? W / 2 : 2 * W;
+  const int tiles_y = (Ho + T::OTY - 1) / T::OTY, tiles_x = (Wo + T::OTX - 1) / T::OTX;
+  const long long n = (long long)B * tiles_y * tiles_x * (C / kCB);
+  if (n <= 0 || n > 0x7fffffffLL) return SNRSE_EINVAL;
+  hipLaunchKernelGGL(gn_resample_kernel<MODE>, dim3((unsigned)n), dim3(256), 0, stream, (const bf16_t*)src, C, H,
+                     W, tiles_x, tiles_y, scale, shift, act, (bf16_t*)out_act, (bf16_t*)out_raw);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int snrse_gn_resample(const void* src, int C, int B, int H, int W, const float* scale,
+                                 const float* shift, int act, int mode, void* out_act, void* out_raw,
+                                 hipStream_t stream) {
+  if (!src || !out_act || C <= 0 || C % kCB || B <= 0 || H <= 0 || W <= 0 || (!scale) != (!shift))
+    return SNRSE_EINVAL;
+  if (mode == MODE_DOWN) {
+    if ((H & 1) || (W & 1)) return SNRSE_EINVAL;
+    return launch_resample<MODE_DOWN>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream);
+  }
+  if (mode == MODE_UP) return launch_resample<MODE_UP>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream);
+  return SNRSE_EINVAL;
+}
+
+extern "C" int snrse_gn_act(const void* src0, int C0, const void* src1, int C1, int B, int HW, const float* scale,
+                            const float* shift, int act, void* out, hipStream_t stream) {
+  const int C = C0 + C1;
+  if (!src0 || !out || C0 <= 0 || C0 % 8 || C1 < 0 || C1 % 8 || (C1 > 0 && !src1) || B <= 0 || HW <= 0 ||
+      (!scale) != (!shift) || C > 4096)
+    return SNRSE_EINVAL;
+  const int LP = C / 8;
+  int ppb = (8 * 256) / LP;  // ~8 vectors per thread
+  if (ppb < 1) ppb = 1;
+  dim3 grid((HW + ppb - 1) / ppb, B);
+  hipLaunchKernelGGL(gn_act_kernel, grid, dim3(256), sizeof(float) * 2 * C, stream, (const bf16_t*)src0, C0,
+                     (const bf16_t*)src1, C1, HW, ppb, scale, shift, act, (bf16_t*)out);
+  return (int)hipGetLastError();
+}

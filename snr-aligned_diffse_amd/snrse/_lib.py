@@ -42,6 +42,9 @@ SIGNATURES = {
     "snrse_spec_transform": [_vp, _vp, C.c_longlong, _i, _vp],
     "snrse_snrnet": [_vp, _i, _i] + [_vp] * 17 + [_vp, _vp, _vp],
     "snrse_istft": [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
+    "snrse_gn_resample": [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp],
+    "snrse_gn_act": [_vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp],
+    "snrse_set_workspace": [_vp, C.c_size_t],
 }
 HOUSEKEEPING = {"snrse_abi_version": ([], _i), "snrse_error_string": ([_i], C.c_char_p),
                 "snrse_device_name": ([C.c_char_p, _i], _i), "snrse_snrnet_workspace": ([_i, _i], C.c_size_t)}

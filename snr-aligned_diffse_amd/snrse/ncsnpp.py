@@ -175,10 +175,16 @@ class NCSNppHIP:
         mode = "up" if m.up else ("down" if m.down else "none")
         (t0, s0), (t1, s1) = x0, (x1 if x1 is not None else (None, None))
         B, H, W, _ = t0.shape
+        xs_raw = None
         if mode == "none" and ops.halo_ok(t0, 3, m.cout):
             gn0 = ops.gn_scale_shift(s0, e["gn0_g"], e["gn0_b"], H * W, sums1=s1)
             h, hs_ = self._conv(t0, e["w0"], 3, m.cout, src1=t1, gn=gn0, bias=e["b0"], temb=dense,
                                 temb_off=e["temb_off"])
+        elif mode != "none" and t1 is None and t0.dtype == torch.bfloat16 and t0.shape[3] % 16 == 0:
+            # one LDS-tiled pass: SiLU(GN(x)) resampled for Conv_0 and the raw FIR of x for Conv_2
+            gn0 = ops.gn_scale_shift(s0, e["gn0_g"], e["gn0_b"], H * W)
+            a0, xs_raw = ops.gn_resample(t0, *gn0, act=True, mode=mode, want_raw="w2" in e)
+            h, hs_ = self._conv(a0, e["w0"], 3, m.cout, bias=e["b0"], temb=dense, temb_off=e["temb_off"])
         else:
             a0 = ops.gn_apply(t0, t1, s0, e["gn0_g"], e["gn0_b"], act=True, mode=mode, sums1=s1)
             h, hs_ = self._conv(a0, e["w0"], 3, m.cout, bias=e["b0"], temb=dense, temb_off=e["temb_off"])
@@ -189,7 +195,7 @@ class NCSNppHIP:
             src, gn1 = ops.gn_apply(h, None, hs_, e["gn1_g"], e["gn1_b"], act=True), None
         if "w2" in e:
             if mode != "none":
-                xs0, xs1 = ops.fir(t0, mode), None
+                xs0, xs1 = (ops.fir(t0, mode) if xs_raw is None else xs_raw), None
             else:
                 xs0, xs1 = t0, t1
             return self._conv(src, e["w1"], 3, m.cout, gn=gn1, bias=e["b1"], sc=xs0, sc1=xs1, sc_wgt=e["w2"],
@@ -209,7 +215,11 @@ class NCSNppHIP:
     def _pyramid_head(self, gn_m, conv_m, h, pyr_up):
         g = self.mw[gn_m.idx]
         c = self.mw[conv_m.idx]
-        a = ops.gn_apply(h[0], None, h[1], g["g"], g["b"], act=True)
+        t, s = h
+        if ops.head_ok(t):  # GroupNorm+SiLU fused into the head conv's halo load
+            gn = ops.gn_scale_shift(s, g["g"], g["b"], t.shape[1] * t.shape[2])
+            return ops.conv2d(t, c["w"], 3, 4, bias=c["b"], res=pyr_up, out_f32=True, gn=gn)
+        a = ops.gn_apply(t, None, s, g["g"], g["b"], act=True)
         return ops.conv2d(a, c["w"], 3, 4, bias=c["b"], res=pyr_up, out_f32=True)
 
     # ------------------------------------------------------------------ forward

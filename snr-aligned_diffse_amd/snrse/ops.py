@@ -6,6 +6,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 
 import torch
 
@@ -31,6 +32,20 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+_WS = {"dev": None, "buf": None}
+
+
+def _workspace(dev):
+    """Register (once per device) the split-K workspace of the small-image GEMMs
+    (snrse_set_workspace); SNRSE_WORKSPACE_MB sizes it, 0 disables K splitting."""
+    if _WS["dev"] == dev:
+        return
+    mb = int(os.environ.get("SNRSE_WORKSPACE_MB", "128"))
+    buf = torch.empty(mb << 18, dtype=torch.float32, device=dev) if mb > 0 else None
+    _lib.call("snrse_set_workspace", None if buf is None else buf.data_ptr(), 0 if buf is None else mb << 20)
+    _WS.update(dev=dev, buf=buf)
+
+
 def _dev(*ts):
     for t in ts:
         if t is not None and not t.is_cuda:
@@ -47,6 +62,7 @@ def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_w
     stats: optional new_stats() buffer receiving the output's per-channel (sum, sumsq).
     gn: optional (scale, shift) [B, C0+C1] f32 — consume SiLU(GN(x)) (halo path only, see halo_ok)."""
     _dev(src0, src1, wgt, sc, sc1, sc_wgt, bias, res, comb, comb_w, comb_b, temb)
+    _workspace(src0.device)
     B, H, W, C0 = src0.shape
     C1 = 0 if src1 is None else src1.shape[3]
     Csc = 0 if sc is None else sc.shape[3]
@@ -72,16 +88,33 @@ def get_option(name):
     return v.value
 
 
+KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 4: "conv_halo_kernel", 5: "conv_halo5_kernel",
+           6: "conv_halo6_kernel", 8: "conv_halo8_kernel", 9: "conv_head_kernel"}
+
+
+def kernel_name(gen):
+    """Kernel symbol of a conv generation code (snrse_get_option "last_kernel" / "halo_kernel")."""
+    return KERNELS.get(gen, f"conv_kernel_{gen}")
+
+
 def conv_kernel_name():
     """Kernel symbol the halo-eligible convs dispatch to under the current setting."""
-    return {6: "conv_halo6_kernel", 5: "conv_halo5_kernel"}.get(get_option("halo_kernel"), "conv_halo_kernel")
+    return kernel_name(get_option("halo_kernel"))
 
 
 def halo_ok(x, ksize, cout):
     """True when snrse_conv2d takes the halo path (and so accepts a fused GroupNorm)."""
     B, H, W, C = x.shape
     return (x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and H % 4 == 0 and W % 64 == 0
-            and _VARIANT["v"] in (0, 4, 5, 6) and x.numel() * 2 < 0x7ff00000)
+            and _VARIANT["v"] in (0, 4, 5, 6, 8) and x.numel() * 2 < 0x7ff00000)
+
+
+def head_ok(x):
+    """True when a bf16 3x3 conv of x with Cout <= 16 and f32 output (the pyramid heads) takes the
+    halo-staged head kernel, which accepts a fused GroupNorm (gn=)."""
+    B, H, W, C = x.shape
+    return (x.dtype == torch.bfloat16 and H % 4 == 0 and W % 64 == 0 and C % 32 == 0 and _VARIANT["v"] != 1
+            and x.numel() * 2 < 0x7ff00000)
 
 
 def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):
@@ -143,11 +176,50 @@ def gn_apply(src0, src1=None, sums=None, gamma=None, beta=None, act=True, mode="
     C1 = 0 if src1 is None else src1.shape[3]
     C = C0 + C1
     m = MODES[mode]
+    if src0.dtype == torch.bfloat16 and sums is not None:
+        # bf16: the per-(b, c) affine once, then the elementwise / LDS-tiled apply
+        scale, shift = gn_scale_shift(sums, gamma, beta, H * W, sums1=sums1, groups=groups, eps=eps)
+        if m == 0:
+            return gn_act(src0, src1, scale, shift, act=act)
+        if src1 is None and C0 % 16 == 0:
+            return gn_resample(src0, scale, shift, act=act, mode=mode)[0]
     Ho, Wo = (H // 2, W // 2) if m == 1 else ((2 * H, 2 * W) if m == 2 else (H, W))
     out = torch.empty(B, Ho, Wo, C, device=src0.device, dtype=src0.dtype)
     g = groups if groups is not None else min(C // 4, 32)
     _lib.call("snrse_gn_apply", _ptr(src0), C0, _ptr(src1), C1, B, H, W, _ptr(sums), _ptr(sums1), _ptr(gamma),
               _ptr(beta), g, float(eps), int(bool(act)), m, out.data_ptr(), code(src0.dtype), _stream())
+    return out
+
+
+def gn_resample(x, scale=None, shift=None, act=True, mode="down", want_raw=False):
+    """act(x*scale+shift) FIR-resampled x2 ('down' / 'up': upfirdn2d with [1,3,3,1]) and, with
+    want_raw, the FIR of x itself (the ResBlock shortcut input) from one LDS-tiled pass over x
+    (snrse_gn_resample; bf16, C % 16 == 0).  Returns (activated, raw or None)."""
+    _dev(x, scale, shift)
+    if x.dtype != torch.bfloat16:
+        raise TypeError("snrse: gn_resample takes bf16 activations")
+    B, H, W, C = x.shape
+    m = MODES[mode]
+    if m == 0:
+        raise ValueError("snrse: gn_resample mode must be 'down' or 'up'")
+    Ho, Wo = (H // 2, W // 2) if m == 1 else (2 * H, 2 * W)
+    oa = torch.empty(B, Ho, Wo, C, device=x.device, dtype=x.dtype)
+    orw = torch.empty_like(oa) if want_raw else None
+    _lib.call("snrse_gn_resample", x.data_ptr(), C, B, H, W, _ptr(scale), _ptr(shift), int(bool(act)), m,
+              oa.data_ptr(), _ptr(orw), _stream())
+    return oa, orw
+
+
+def gn_act(src0, src1=None, scale=None, shift=None, act=True):
+    """act(x*scale+shift) of the channel concatenation (src0 | src1), NHWC bf16 (snrse_gn_act)."""
+    _dev(src0, src1, scale, shift)
+    if src0.dtype != torch.bfloat16:
+        raise TypeError("snrse: gn_act takes bf16 activations")
+    B, H, W, C0 = src0.shape
+    C1 = 0 if src1 is None else src1.shape[3]
+    out = torch.empty(B, H, W, C0 + C1, device=src0.device, dtype=src0.dtype)
+    _lib.call("snrse_gn_act", src0.data_ptr(), C0, _ptr(src1), C1, B, H * W, _ptr(scale), _ptr(shift),
+              int(bool(act)), out.data_ptr(), _stream())
     return out
 
 

@@ -33,14 +33,14 @@ def nchw(x):
 DT = {"f32": (torch.float32, 2e-6), "bf16": (torch.bfloat16, 1e-2)}
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 4, 5, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 5, 6, 8])
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 16), (1, 256, 128, 4, 8), (3, 128, 256, 5, 7), (2, 384, 256, 4, 4),
                                    (2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (1, 256, 256, 12, 64)])
 def test_conv3x3(gpu, dt, shape, variant):
     """variant: 0 auto (persistent halo kernel where H%4==0, W%64==0), 1 register-staged, 2 LDS-DMA
     im2col, 4 halo v4 with the register epilogue, 5 halo v5 (two workgroups per CU), 6 persistent
-    halo v6 (falls back to v4 outside its contract)."""
+    halo v6 (falls back to v4 outside its contract), 8 ping-pong halo v8 (falls back to v5)."""
     from snrse import ops
     dtype, tol = DT[dt]
     B, cin, cout, H, W = shape
@@ -324,7 +324,7 @@ def test_philox_noise_statistics(gpu):
 
 
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (2, 256, 128, 4, 64)])
-@pytest.mark.parametrize("variant", [0, 4, 5])
+@pytest.mark.parametrize("variant", [0, 4, 5, 8])
 def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     """Halo GEMM consuming SiLU(GN(x)) from raw x + per-(b,c) scale/shift (+ raw 1x1 shortcut)."""
     from snrse import ops
@@ -362,11 +362,12 @@ def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     (8, 256, 0, 256, 64, 128, 0, 0, True, True, False, True),      # two Cout tiles per image
     (2, 256, 256, 256, 32, 64, 0, 0, False, False, True, False),   # cat input, no GN, fewer tiles than workgroups
 ])
-def test_conv_halo6_persistent(gpu, case):
-    """Persistent halo GEMM (v6) vs an fp32 torch reference on the GPU at sizes where every
-    workgroup runs several tiles (the pipeline crosses chunk, tile and image boundaries),
-    with the fused GroupNorm+SiLU prologue, cat inputs, the 1x1 shortcut, temb, residual
-    and the per-channel output statistics."""
+@pytest.mark.parametrize("variant", [6, 8])
+def test_conv_halo_persistent(gpu, case, variant):
+    """Persistent halo GEMMs (v6; v8, which hands shortcut convs to v5) vs an fp32 torch reference
+    on the GPU at sizes where every workgroup runs several tiles (the pipeline crosses chunk, tile
+    and image boundaries), with the fused GroupNorm+SiLU prologue, cat inputs, the 1x1 shortcut,
+    temb, residual and the per-channel output statistics."""
     from snrse import ops
     B, C0, C1, Co, H, W, Csc, Csc1, use_gn, use_temb, use_res, use_st = case
     g = torch.Generator(device=gpu).manual_seed(sum(case[:8]))
@@ -400,17 +401,105 @@ def test_conv_halo6_persistent(gpu, case):
         ref = ref + res.float().permute(0, 3, 1, 2)
     ref = ref * scale
     st = ops.new_stats(B, Co) if use_st else None
-    ops.set_option("conv_variant", 6)
+    ops.set_option("conv_variant", variant)
     try:
-        assert ops.conv_kernel_name() == "conv_halo6_kernel"
         out = ops.conv2d(x0, w.reshape(Co, -1).contiguous(), 3, Co, bias=bias, src1=x1, sc=xs0, sc1=xs1, sc_wgt=ws,
                          temb=temb, temb_off=40, res=res, out_scale=scale, stats=st, gn=gn)
+        ran = ops.kernel_name(ops.get_option("last_kernel"))
         torch.cuda.synchronize()
     finally:
         ops.set_option("conv_variant", 0)
+    expect = "conv_halo6_kernel" if variant == 6 else ("conv_halo5_kernel" if Csc else "conv_halo8_kernel")
+    assert ran == expect
     got = out.float().permute(0, 3, 1, 2)
     assert rel(got, ref) < 1e-2
     if use_st:
         o = out.double()
         st_ref = torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)
         assert rel(ops.fold_stats(st), st_ref) < 3e-3
+
+
+@pytest.mark.parametrize("mode", ["down", "up"])
+@pytest.mark.parametrize("shape", [(2, 128, 8, 16), (1, 256, 36, 70), (3, 16, 18, 34), (1, 32, 9, 21)])
+def test_gn_resample_tiled(gpu, mode, shape):
+    """LDS-tiled GroupNorm+SiLU+FIR and, in the same pass, the raw FIR of the shortcut input
+    (layerspp.py:245-257), with partial tiles at the image edges, against the oracle FIR applied to
+    an fp64 GroupNorm+SiLU."""
+    from snrse import ops
+    B, C, H, W = shape
+    if mode == "down" and (H % 2 or W % 2):
+        pytest.skip("down-sampling needs even H and W")
+    x = (torch.from_numpy(fnormal("t.rs.x", (B, C, H, W))) * 2 + 0.3).bfloat16().float()
+    g = torch.from_numpy(fnormal("t.rs.g", (C,))) * 0.1 + 1
+    be = torch.from_numpy(fnormal("t.rs.b", (C,))) * 0.1
+    fir = ncsnpp_ref.fir_down2 if mode == "down" else ncsnpp_ref.fir_up2
+    ref_a = fir(F.silu(F.group_norm(x.double(), min(C // 4, 32), g.double(), be.double(), eps=1e-6)))
+    ref_r = fir(x.double())
+    xg = nhwc(x).to(gpu, torch.bfloat16)
+    sums, _ = ops.gn_stats(xg)
+    scale, shift = ops.gn_scale_shift(sums, g.to(gpu), be.to(gpu), H * W)
+    a, r = ops.gn_resample(xg, scale, shift, act=True, mode=mode, want_raw=True)
+    assert rel(nchw(a.float()), ref_a) < 1e-2
+    assert rel(nchw(r.float()), ref_r) < 1e-2
+
+
+@pytest.mark.parametrize("out_f32", [False, True])
+def test_conv_splitk_small_levels(gpu, out_f32):
+    """Small-image convs (the tile grid underfills the CUs) run as split-K GEMMs whose fp32 partial
+    sums land in the registered workspace and are finished by conv_splitk_finalize (bias, temb,
+    residual, scale, GroupNorm statistics); they must agree with the unsplit GEMM and with fp64."""
+    from snrse import ops
+    B, C0, C1, cout, H, W = 4, 256, 256, 256, 8, 16
+    x = torch.from_numpy(fnormal("t.sk.x", (B, C0 + C1, H, W))).bfloat16().float()
+    w = (torch.from_numpy(fnormal("t.sk.w", (cout, C0 + C1, 3, 3))) / 68).bfloat16().float()
+    b = torch.from_numpy(fnormal("t.sk.b", (cout,)))
+    temb = torch.from_numpy(fnormal("t.sk.t", (B, 300)))
+    odt = torch.float32 if out_f32 else torch.bfloat16
+    r = torch.from_numpy(fnormal("t.sk.r", (B, cout, H, W))).to(odt).float()
+    ref = (F.conv2d(x.double(), w.double(), b.double(), padding=1) + temb[:, 8:8 + cout, None, None].double()
+           + r.double()) * 0.5
+    xg = nhwc(x).to(gpu, torch.bfloat16)
+    wp = w.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu, torch.bfloat16).contiguous()
+    outs = {}
+    for sk in (0, 1):
+        ops.set_option("splitk", sk)
+        try:
+            st = ops.new_stats(B, cout)
+            o = ops.conv2d(xg[..., :C0].contiguous(), wp, 3, cout, bias=b.to(gpu), src1=xg[..., C0:].contiguous(),
+                           temb=temb.to(gpu), temb_off=8, res=nhwc(r).to(gpu, odt), out_scale=0.5, out_f32=out_f32,
+                           stats=st)
+            outs[sk] = (o, st, ops.get_option("last_ksplit"))
+        finally:
+            ops.set_option("splitk", 1)
+    assert outs[0][2] == 1 and outs[1][2] > 1
+    for o, st, _ in outs.values():
+        assert rel(nchw(o.float()), ref) < 1e-2
+        od = o.double()
+        st_ref = torch.stack([od.sum((1, 2)), (od * od).sum((1, 2))], -1)
+        assert rel(ops.fold_stats(st), st_ref) < 3e-3
+    assert rel(outs[1][0].float(), outs[0][0].float()) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 128, 8, 64), (1, 256, 4, 128), (2, 128, 12, 64)])
+def test_conv_head_fused_groupnorm(gpu, shape):
+    """Pyramid-head conv (C -> 4, f32 out, + upsampled pyramid) consuming SiLU(GN(h)) through the
+    halo-staged head kernel (ncsnpp.py:348-366)."""
+    from snrse import ops
+    B, C, H, W = shape
+    x = (torch.from_numpy(fnormal("t.hd.x", (B, C, H, W))) * 1.5 + 0.2).bfloat16().float()
+    w = (torch.from_numpy(fnormal("t.hd.w", (4, C, 3, 3))) / 48).bfloat16().float()
+    b = torch.from_numpy(fnormal("t.hd.b", (4,)))
+    r = torch.from_numpy(fnormal("t.hd.r", (B, 4, H, W)))
+    g = torch.from_numpy(fnormal("t.hd.g", (C,))) * 0.1 + 1
+    be = torch.from_numpy(fnormal("t.hd.be", (C,))) * 0.1
+    a = F.silu(F.group_norm(x.double(), min(C // 4, 32), g.double(), be.double(), eps=1e-6))
+    ref = F.conv2d(a, w.double(), b.double(), padding=1) + r.double()
+    xg = nhwc(x).to(gpu, torch.bfloat16)
+    sums, _ = ops.gn_stats(xg)
+    gn = ops.gn_scale_shift(sums, g.to(gpu), be.to(gpu), H * W)
+    wp = torch.cat([w.permute(0, 2, 3, 1).reshape(4, -1), torch.zeros(12, 9 * C)]).to(gpu, torch.bfloat16).contiguous()
+    assert ops.head_ok(xg)
+    out = ops.conv2d(xg, wp, 3, 4, bias=b.to(gpu), res=nhwc(r).to(gpu), out_f32=True, gn=gn)
+    assert ops.kernel_name(ops.get_option("last_kernel")) == "conv_head_kernel"
+    assert out.dtype == torch.float32
+    assert rel(nchw(out), ref) < 1e-2
