@@ -7,7 +7,7 @@
 //             = acc[2][4][4] of 16x16x32 MFMAs with A = weights, B = halo pixels (D[co][px])
 //   phase   = one tap of one 32-channel K chunk: an L section (12 fragment ds_reads, one 1-KB weight
 //             LDS-DMA piece for three phases ahead, at taps 0..2 two pieces of the next chunk's halo,
-//             at taps 4..8 the in-place GroupNorm(+SiLU) of that halo), a barrier, an M section
+//             at taps 5..8 the in-place GroupNorm(+SiLU) of that halo), a barrier, an M section
 //             (32 MFMAs), a barrier.  Waves 4..7 run one barrier behind waves 0..3, so on every SIMD
 //             one wave's L section runs beside the other wave's MFMAs.
 //   halo    = two buffers of (8+2) x (64+2) rows x 64 B (32 channels); row image hy * 66 + hx, 16-B
@@ -21,6 +21,8 @@
 // in-loop wait is an exact counted vmcnt (k8_wait_vm).  Epilogue: the accumulators of channel
 // blocks (2jp, 2jp+1) are exchanged between DPP rows (v_permlane16_swap), so every lane holds 8
 // consecutive channels of one pixel: 16-B residual loads and 16-B stores.
+#include <stdlib.h>
+
 #include "conv_common.h"
 
 namespace snrse_conv {
@@ -67,14 +69,13 @@ SNRSE_DEV float k8_row_sum16(float v) {
   return v;
 }
 // the L section's closing wait: retire the weight slice the next phase reads (issued two phases
-// before), and at tap 3 the halo pieces issued at taps 0..2 (the GroupNorm pass reads them from tap 4)
+// before), and at tap 4 the halo pieces issued at taps 0..2 (the GroupNorm pass reads them from tap 5:
+// an HBM-missing halo piece takes several phases to land)
 template <int TP>
 SNRSE_DEV void k8_wait_vm() {
   if constexpr (TP == 0) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (TP == 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (TP == 1 || TP == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (TP == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (TP == 3) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  else if constexpr (TP == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
 }
 
@@ -82,15 +83,23 @@ struct Tile8 {
   int b, h0, w0, n0;
 };
 
-__global__ __launch_bounds__(512, 1) void conv_halo8_kernel(ConvParams p, int T) {
+__global__ __launch_bounds__(512, 1) void conv_halo8_kernel(ConvParams p, int T, int stagger) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wid >> 2;
+#ifdef SNRSE_STAMPS
+  unsigned long long* const lst = (unsigned long long*)(smem + K8_LDS) + wid * 32;
+#endif
+  SNRSE_STAMP(0);
   const int G = gridDim.x, g = blockIdx.x;
   const int t_begin = (int)(((long long)g * T) / G);
   const int ntile = (int)(((long long)(g + 1) * T) / G) - t_begin;
   if (ntile <= 0) return;
+  // odd workgroups start about half a tile late, so the CUs' epilogue store bursts do not coincide
+  if (g & 1) {
+    for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   const int Cin = p.C0 + p.C1, ncm = Cin >> 5, K1 = 9 * Cin;
   const int ntw = p.W / K8_TW, nth = p.H / K8_TH;
   const bool has_gn = p.gn_scale != nullptr;
@@ -210,10 +219,14 @@ __global__ __launch_bounds__(512, 1) void conv_halo8_kernel(ConvParams p, int T)
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  SNRSE_STAMP(1);
   if (grp == 1) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half wins VALU arbitration
 
   int hb = 0, slot = 0;
   const int sslot = blockIdx.x & (SNRSE_STAT_SLOTS - 1);
+  // true for the first two phases after the prologue / an epilogue: the weights they wait for were
+  // drained before it, so they skip their vmcnt and do not wait on the epilogue's stores
+  bool fresh = true;
 #pragma unroll 1
   for (int lt = 0; lt < ntile; ++lt) {
     const bool has_nt = lt + 1 < ntile;
@@ -227,9 +240,20 @@ __global__ __launch_bounds__(512, 1) void conv_halo8_kernel(ConvParams p, int T)
       const int cx = has_next ? (last_c ? 0 : c + 1) : c;     // (re-fetch of this one past the end)
       const bool next_gn = has_gn && has_next;
       const int hbo = hb * K8_HBUF, hbn = hb ^ 1;
+#if defined(SNRSE_STAMPS) && defined(SNRSE_STAMPS_PHASE)
+#define K8_PSTAMP(I)                            \
+  do {                                          \
+    if (lt == 0 && c == 1 && tp_ < 6) SNRSE_STAMP(I); \
+  } while (0)
+#else
+#define K8_PSTAMP(I) \
+  do {               \
+  } while (0)
+#endif
 #define K8_PHASE(TP)                                                                                         \
   do {                                                                                                       \
     constexpr int tp_ = (TP);                                                                                \
+    K8_PSTAMP(2 + 4 * tp_);                                                                                  \
     u32x4 bh[4], aw[8];                                                                                      \
     _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                            \
       bh[i] = *(const u32x4*)(smem + hoff[tp_ % 3] + hbo + (tp_ / 3) * K8_HROWB + i * 1024);                         \
@@ -239,26 +263,30 @@ __global__ __launch_bounds__(512, 1) void conv_halo8_kernel(ConvParams p, int T)
     else if (has_next) w_issue(tx, cx, tp_ - 6, (slot + 3) & 3);                                             \
     else w_issue(tc, c, tp_, (slot + 3) & 3);                                                                \
     if constexpr (tp_ < 3) halo_issue(tx, cx, hbn, tp_);                                                     \
-    if constexpr (tp_ >= 4) {                                                                                \
+    if constexpr (tp_ >= 5) {                                                                                \
       if (next_gn) {                                                                                         \
-        trans_row(tx, hbn, tp_ - 4);                                                                         \
-        if constexpr (tp_ == 8) trans_row(tx, hbn, 5);                                                       \
+        trans_row(tx, hbn, tp_ == 5 ? 0 : (tp_ == 6 ? 1 : 2 * tp_ - 12));                                     \
+        if constexpr (tp_ >= 7) trans_row(tx, hbn, 2 * tp_ - 11);                                            \
       }                                                                                                      \
     }                                                                                                        \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                       \
-    k8_wait_vm<tp_>();                                                                                       \
+    if (tp_ > 1 || !fresh) k8_wait_vm<tp_>();                                                                \
+    K8_PSTAMP(3 + 4 * tp_);                                                                                  \
     __builtin_amdgcn_s_barrier();                                                                            \
+    K8_PSTAMP(4 + 4 * tp_);                                                                                  \
     __builtin_amdgcn_sched_barrier(0);                                                                       \
     _Pragma("unroll") for (int h = 0; h < 2; ++h)                                                            \
       _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                          \
         _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                        \
           acc[h][i][j] = mfma_chunk<bf16_t>(aw[h * 4 + j], bh[i], acc[h][i][j]);                              \
     __builtin_amdgcn_sched_barrier(0);                                                                       \
+    K8_PSTAMP(5 + 4 * tp_);                                                                                  \
     __builtin_amdgcn_s_barrier();                                                                            \
     slot = (slot + 1) & 3;                                                                                   \
   } while (0)
       K8_PHASE(0);
       K8_PHASE(1);
+      fresh = false;
       K8_PHASE(2);
       K8_PHASE(3);
       K8_PHASE(4);
@@ -267,10 +295,15 @@ __global__ __launch_bounds__(512, 1) void conv_halo8_kernel(ConvParams p, int T)
       K8_PHASE(7);
       K8_PHASE(8);
 #undef K8_PHASE
+#undef K8_PSTAMP
       hb = hbn;
     }
     if (grp == 0) __builtin_amdgcn_s_barrier();  // re-align the two wave groups
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    fresh = true;
+#if defined(SNRSE_STAMPS) && !defined(SNRSE_STAMPS_PHASE)
+    if (lt < 13) SNRSE_STAMP(2 + 2 * lt);
+#endif
 
     // ---- epilogue: exchange channel blocks (2jp, 2jp+1) between DPP rows (lg even <-> lg odd), so
     // lane (lrow, lg) holds channels cl .. cl+7, cl = 64 h + 16 (2 jp + (lg & 1)) + 8 (lg >> 1), of
@@ -366,6 +399,9 @@ __global__ __launch_bounds__(512, 1) void conv_halo8_kernel(ConvParams p, int T)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
+#if defined(SNRSE_STAMPS) && !defined(SNRSE_STAMPS_PHASE)
+    if (lt < 13) SNRSE_STAMP(3 + 2 * lt);
+#endif
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -374,6 +410,26 @@ __global__ __launch_bounds__(512, 1) void conv_halo8_kernel(ConvParams p, int T)
         for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     tc = tn;
   }
+  SNRSE_STAMP(28);
+#ifdef SNRSE_STAMPS
+  {
+    unsigned long long st_[29];
+    if (lane == 0)
+      for (int i = 0; i < 29; ++i) st_[i] = lst[i];
+    unsigned long long t_end;
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_end)::"memory");
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (lane == 0 && p.stamps) {
+      unsigned long long* gs = p.stamps + ((size_t)blockIdx.x * 8 + wid) * 32;
+      for (int i = 0; i < 29; ++i) gs[i] = st_[i];
+      gs[29] = t_end;
+      gs[30] = hw;
+      gs[31] = xcc;
+    }
+  }
+#endif
 }
 
 }  // namespace
@@ -397,16 +453,26 @@ int launch_halo8(const ConvParams& p0, hipStream_t s) {
   if (!halo8_ok(p)) return SNRSE_EINVAL;
   p.ntn = p.Cout / 128;
   const int T = p.B * (p.H / K8_TH) * (p.W / K8_TW) * p.ntn;
+#ifdef SNRSE_STAMPS
+  constexpr size_t lds = K8_LDS + 8 * 32 * 8;
+#else
+  constexpr size_t lds = K8_LDS;
+#endif
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
     SNRSE_RET(hipGetDevice(&dev));
     SNRSE_RET(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     SNRSE_RET(hipFuncSetAttribute((const void*)conv_halo8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)K8_LDS));
+                                  (int)lds));
   }
   const int G = T < ncu ? T : ncu;
-  hipLaunchKernelGGL(conv_halo8_kernel, dim3(G), dim3(512), K8_LDS, s, p, T);
+  // half a tile (~1.3k cycles per phase, 9 phases per 32-channel chunk, ~17k epilogue; s_sleep 127
+  // ~8k cycles) when every workgroup runs enough tiles to amortise it; SNRSE_K8_STAGGER=0 disables
+  static const int stagger_on = getenv("SNRSE_K8_STAGGER") ? atoi(getenv("SNRSE_K8_STAGGER")) : 1;
+  const int ncm = (p.C0 + p.C1) / 32;
+  const int stagger = (stagger_on && T >= 8 * G) ? (ncm * 9 * 1300 + 17000) / 2 / 8128 : 0;
+  hipLaunchKernelGGL(conv_halo8_kernel, dim3(G), dim3(512), lds, s, p, T, stagger);
   return (int)hipGetLastError();
 }
 

@@ -30,20 +30,45 @@ def _gn_pair(B, C, dev, g):
     return ss[0], ss[1]
 
 
+PHASE_LIB = os.path.join(PKG, "lib", "stamps_phase", "libsnrse_hip.so")
+
+
 def build():
     from snrse import build as b
-    os.makedirs(os.path.dirname(STAMP_LIB), exist_ok=True)
-    print(b.build_library(force=True, extra_flags=("-DSNRSE_STAMPS",), lib=STAMP_LIB))
+    for lib, flags in ((STAMP_LIB, ("-DSNRSE_STAMPS",)), (PHASE_LIB, ("-DSNRSE_STAMPS", "-DSNRSE_STAMPS_PHASE"))):
+        os.makedirs(os.path.dirname(lib), exist_ok=True)
+        print(b.build_library(force=True, extra_flags=flags, lib=lib))
 
 
-def v6_report(s, shape, ms):
-    """v6 stamps: 0 start, 1 prologue done, 2+2t / 3+2t epilogue start / end of local tile t
-    (t < 13), 28 loop end, 29 kernel end; 4 waves per workgroup."""
+def v8_phase_report(s, shape, ms):
+    """v8 phase stamps (-DSNRSE_STAMPS_PHASE): chunk 1 of each workgroup's first tile, taps 0..5:
+    2+4t L start, 3+4t L end (before barrier 1), 4+4t after barrier 1, 5+4t M end; per wave group."""
     import numpy as np
-    s = s[:, :4]
+    s = s[:, :8]
+    s = s[s[:, 0, 29] != 0]
+    out = {"shape": shape, "variant": 8, "ms": ms, "phase_stamps": True}
+    for gname, ws in (("waves0-3", slice(0, 4)), ("waves4-7", slice(4, 8))):
+        g = s[:, ws]
+        rows = []
+        for t in range(6):
+            L = (g[:, :, 3 + 4 * t] - g[:, :, 2 + 4 * t]).mean()
+            b1 = (g[:, :, 4 + 4 * t] - g[:, :, 3 + 4 * t]).mean()
+            M = (g[:, :, 5 + 4 * t] - g[:, :, 4 + 4 * t]).mean()
+            b2 = (g[:, :, 2 + 4 * (t + 1)] - g[:, :, 5 + 4 * t]).mean() if t < 5 else float("nan")
+            rows.append({"tap": t, "L": round(float(L)), "wait_b1": round(float(b1)), "M": round(float(M)),
+                         "wait_b2": round(float(b2)) if t < 5 else None})
+        out[gname] = rows
+    return out
+
+
+def v6_report(s, shape, ms, nw=4, variant=6):
+    """v6 / v8 stamps: 0 start, 1 prologue done, 2+2t / 3+2t epilogue start / end of local tile t
+    (t < 13), 28 loop end, 29 kernel end; nw waves per workgroup (v6: 4, v8: 8)."""
+    import numpy as np
+    s = s[:, :nw]
     s = s[s[:, 0, 29] != 0]
     rel = s - s[:, :, :1]
-    out = {"shape": shape, "variant": 6, "ms": ms, "workgroups": int(s.shape[0]),
+    out = {"shape": shape, "variant": variant, "ms": ms, "workgroups": int(s.shape[0]),
            "wave_total_mean": float(rel[:, :, 29].mean()), "prologue": float(rel[:, :, 1].mean())}
     mains, epis = [], []
     prev = rel[:, :, 1]
@@ -70,10 +95,11 @@ def main():
     ap.add_argument("--variants", default="0")
     ap.add_argument("--stats", default="1", help="comma list of 0/1: fuse GN statistics")
     ap.add_argument("--gn", action="store_true", help="fused GroupNorm+SiLU prologue")
+    ap.add_argument("--phase", action="store_true", help="v8 phase-level stamp build")
     a = ap.parse_args()
     if a.build:
         return build()
-    os.environ["SNRSE_LIB"] = STAMP_LIB
+    os.environ["SNRSE_LIB"] = PHASE_LIB if a.phase else STAMP_LIB
     import numpy as np
     import torch
     from snrse import _lib, ops
@@ -115,8 +141,11 @@ def main():
             lib.snrse_debug_set_stamps(None)
             ms = e0.elapsed_time(e1)
             s = buf.view(nblk, 8, 32).cpu().numpy().astype(np.int64)
-            if v == 6:
-                print(json.dumps(v6_report(s, SHAPES[si], ms)), flush=True)
+            if v == 8 and a.phase:
+                print(json.dumps(v8_phase_report(s, SHAPES[si], ms)), flush=True)
+                continue
+            if v in (6, 8):
+                print(json.dumps(v6_report(s, SHAPES[si], ms, nw=4 if v == 6 else 8, variant=v)), flush=True)
                 continue
             s = s[:, :4] if v == 5 else s  # v5 workgroups have 4 waves
             cin = C0 + C1
