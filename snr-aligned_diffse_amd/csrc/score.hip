@@ -53,27 +53,47 @@ __global__ __launch_bounds__(512) void temb_mlp_kernel(const float* t, const flo
 }
 
 // out[b][r] = W[r] . silu(temb[b]) + bias[r];  block: 256 threads = 4 waves, 16 rows per wave
+// out[b][r] = bias[r] + sum_d W[r][d] * silu(temb[b][d]).  Block = 4 waves x 64 rows (lane = row);
+// wave w accumulates images w, w+4, ...; W is read in 64-wide d chunks straight into registers
+// (16-B loads per lane), SiLU(temb) is staged in LDS and read as wave-uniform broadcasts.
 __global__ __launch_bounds__(256) void temb_dense_kernel(const float* temb, const float* W, const float* bias,
                                                          float* out, int B, int R, int D) {
-  extern __shared__ float st[];  // [B][D] silu(temb)
+  extern __shared__ __attribute__((aligned(16))) float st[];  // [B][D] silu(temb)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int i = tid; i < B * D; i += 256) st[i] = silu_exact(temb[i]);
   __syncthreads();
-  const int r0 = blockIdx.x * 64 + wid * 16;
-  for (int rr = 0; rr < 16; ++rr) {
-    const int r = r0 + rr;
-    if (r >= R) break;
-    const float* w = W + (size_t)r * D;
-    float wv[8];
+  const int r = blockIdx.x * 64 + lane;
+  const bool rok = r < R;
+  float acc[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) wv[i] = (lane + 64 * i < D) ? w[lane + 64 * i] : 0.f;
-    for (int b = 0; b < B; ++b) {
-      float acc = 0.f;
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  for (int d0 = 0; d0 < D; d0 += 64) {
+    f32x4 w[16];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (lane + 64 * i < D) acc = fmaf(wv[i], st[b * D + lane + 64 * i], acc);
-      acc = wave_sum(acc);
-      if (lane == 0) out[(size_t)b * R + r] = acc + bias[r];
+    for (int q = 0; q < 16; ++q)
+      w[q] = (rok && d0 + 4 * q < D) ? *(const f32x4*)(W + (size_t)r * D + d0 + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int b = wid + 4 * k;
+      if (b < B) {
+        const float* sb = st + b * D + d0;
+        float a = acc[k];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          if (d0 + 4 * q < D) {
+            const f32x4 sv = *(const f32x4*)(sb + 4 * q);
+            a = fmaf(w[q][0], sv[0], fmaf(w[q][1], sv[1], fmaf(w[q][2], sv[2], fmaf(w[q][3], sv[3], a))));
+          }
+        }
+        acc[k] = a;
+      }
+    }
+  }
+  if (rok) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int b = wid + 4 * k;
+      if (b < B) out[(size_t)b * R + r] = acc[k] + bias[r];
     }
   }
 }
@@ -233,7 +253,7 @@ extern "C" int snrse_temb_mlp(const float* t, const float* Wg, const float* W1, 
 
 extern "C" int snrse_temb_dense(const float* temb, const float* W, const float* bias, float* out, int B, int R,
                                 int D, hipStream_t s) {
-  if (D > 512 || B <= 0 || (size_t)B * D * 4 > 64 * 1024) return SNRSE_EINVAL;
+  if (D > 512 || D % 4 || B <= 0 || B > 32 || (size_t)B * D * 4 > 64 * 1024) return SNRSE_EINVAL;
   hipLaunchKernelGGL(temb_dense_kernel, dim3((R + 63) / 64), dim3(256), sizeof(float) * B * D, s, temb, W, bias,
                      out, B, R, D);
   return (int)hipGetLastError();
