@@ -108,10 +108,12 @@ int snrse_set_workspace(void* ptr, size_t bytes);
 /* Tuning switches (A/B experiments): "conv_variant" 0 auto, 1 register-staged v1, 2 LDS-DMA v2,
  * 4 halo kernel v4 with the register epilogue, 5 halo kernel v5 (two workgroups per CU), 6
  * persistent halo v6, 8 ping-pong halo v8 (6 / 8 fall back to 4 / 5 outside their contract);
- * "splitk" 0 disables the split-K small-image GEMMs. */
+ * "splitk" 0 disables the split-K small-image GEMMs; "stats_zeroed" 1 = the statistics buffers
+ * handed to snrse_conv2d / snrse_gn_stats are already zero (the caller clears one arena per network
+ * evaluation), so they skip their per-call memset. */
 int snrse_set_option(const char* name, int value);
 
-/* Read back a switch: "conv_variant", "splitk", "halo_kernel" = generation of the halo conv kernel
+/* Read back a switch: "conv_variant", "splitk", "stats_zeroed", "halo_kernel" = generation of the halo conv kernel
  * the current setting dispatches to (4, 5, 6, 8), "last_kernel" = generation of the most recent
  * snrse_conv2d launch (1 v1, 2 v2, 4/5/6/8 halo, 9 pyramid head), "last_ksplit" = K splits of the
  * most recent v2 launch. */

@@ -18,3 +18,7 @@ extern "C" int snrse_device_name(char* buf, int len) {
   if (len > 0) buf[i] = 0;
   return 0;
 }
+
+// Library-wide switch behind the "stats_zeroed" option (declared in common.h, set through
+// snrse_set_option in conv.hip): statistics buffers arrive already zeroed.
+__attribute__((visibility("hidden"))) int g_snrse_stats_zeroed = 0;

@@ -72,6 +72,9 @@ enum { SNRSE_F32 = 0, SNRSE_BF16 = 1 };
 // their atomics over the slots (a few hundred workgroups per image would otherwise queue on
 // the same 2*C addresses), consumers sum the slots.
 #define SNRSE_STAT_SLOTS 16
+// Option "stats_zeroed" (snrse_set_option): when 1 the caller hands over statistics buffers it
+// has already zeroed (one fill of a per-evaluation arena instead of a memset per producer).
+extern __attribute__((visibility("hidden"))) int g_snrse_stats_zeroed;
 SNRSE_DEV size_t stat_idx(int b, int slot, int c, int C) {
   return (((size_t)b * SNRSE_STAT_SLOTS + slot) * C + c) * 2;
 }

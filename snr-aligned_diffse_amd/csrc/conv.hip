@@ -1402,7 +1402,7 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
   p.wbytes = (long long)npad * ksize * ksize * (C0 + C1) * esz;
   p.sc_wbytes = (long long)npad * (p.Csc + p.Csc1) * esz;
   p.ntn = 1;
-  if (stats) SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * Cout, stream));
+  if (stats && !g_snrse_stats_zeroed) SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * Cout, stream));
   if (dtype == SNRSE_BF16) {
     return out_f32 ? dispatch_conv<bf16_t, float>(p, stream) : dispatch_conv<bf16_t, bf16_t>(p, stream);
   }
@@ -1433,6 +1433,7 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   }
   if (name_is(name, "last_kernel")) { *value = g_last_kernel; return 0; }
   if (name_is(name, "splitk")) { *value = g_splitk; return 0; }
+  if (name_is(name, "stats_zeroed")) { *value = g_snrse_stats_zeroed; return 0; }
   if (name_is(name, "last_ksplit")) { *value = g_last_ksplit; return 0; }
   return SNRSE_EINVAL;
 }
@@ -1441,6 +1442,7 @@ extern "C" int snrse_set_option(const char* name, int value) {
   if (!name) return SNRSE_EINVAL;
   if (name_is(name, "conv_variant")) { g_conv_variant = value; return 0; }
   if (name_is(name, "splitk")) { g_splitk = value; return 0; }
+  if (name_is(name, "stats_zeroed")) { g_snrse_stats_zeroed = value ? 1 : 0; return 0; }
   return SNRSE_EINVAL;
 }
 

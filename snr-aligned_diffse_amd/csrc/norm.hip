@@ -272,8 +272,8 @@ extern "C" int snrse_gn_stats(const void* src0, int C0, const void* src1, int C1
   const int V = dtype == SNRSE_BF16 ? 8 : 4;
   const int C = C0 + C1;
   if (C % V || C0 % V || C / V > 256 || !sums || (C1 > 0 && !sums1)) return SNRSE_EINVAL;
-  SNRSE_RET(hipMemsetAsync(sums, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * C0 * B, stream));
-  if (C1 > 0) SNRSE_RET(hipMemsetAsync(sums1, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * C1 * B, stream));
+  if (!g_snrse_stats_zeroed) SNRSE_RET(hipMemsetAsync(sums, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * C0 * B, stream));
+  if (C1 > 0 && !g_snrse_stats_zeroed) SNRSE_RET(hipMemsetAsync(sums1, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * C1 * B, stream));
   int nblk = (HW + 1023) / 1024;
   if (nblk > 256) nblk = 256;
   const int ppb = (HW + nblk - 1) / nblk;

@@ -98,30 +98,44 @@ __global__ __launch_bounds__(256) void temb_dense_kernel(const float* temb, cons
   }
 }
 
+// One lane per 16-byte chunk of a pixel's 64-channel im2col row (NCH = 64 / VEC chunks per pixel),
+// so a wave's stores are contiguous 16-B vectors; chunk k holds channels k*VEC .. k*VEC+VEC-1,
+// i.e. taps (k*VEC)/4 .. of the 4 real input channels (x.re, x.im, y.re, y.im), zero past tap 8.
 template <typename T>
 __global__ __launch_bounds__(256) void input_pack_kernel(const float2* x, const float2* y, int H, int W,
                                                          T* col, float* pyr, int total) {
-  const int p = blockIdx.x * 256 + threadIdx.x;
+  constexpr int VEC = 16 / sizeof(T), NCH = 64 / VEC;
+  const long long gi = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int p = (int)(gi / NCH), k = (int)(gi % NCH);
   if (p >= total) return;
   const int HW = H * W;
   const int b = p / HW, rem = p - b * HW, h = rem / W, w = rem - (rem / W) * W;
-  const float2 xv = x[p], yv = y[p];
-  float4 pv = make_float4(xv.x, xv.y, yv.x, yv.y);
-  *(float4*)(pyr + (size_t)p * 4) = pv;
-  T* dst = col + (size_t)p * 64;
-  float v[64];
+  if (k == 0) {
+    const float2 xv = x[p], yv = y[p];
+    *(float4*)(pyr + (size_t)p * 4) = make_float4(xv.x, xv.y, yv.x, yv.y);
+  }
+  float v[VEC];
 #pragma unroll
-  for (int i = 0; i < 64; ++i) v[i] = 0.f;
+  for (int i = 0; i < VEC; ++i) v[i] = 0.f;
 #pragma unroll
-  for (int tap = 0; tap < 9; ++tap) {
+  for (int jt = 0; jt < VEC / 4; ++jt) {
+    const int tap = (k * VEC) / 4 + jt;
+    if (tap >= 9) break;
     const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
     if (hh < 0 || hh >= H || ww < 0 || ww >= W) continue;
     const size_t q = (size_t)b * HW + (size_t)hh * W + ww;
     const float2 a = x[q], c = y[q];
-    v[tap * 4 + 0] = a.x; v[tap * 4 + 1] = a.y; v[tap * 4 + 2] = c.x; v[tap * 4 + 3] = c.y;
+    v[jt * 4 + 0] = a.x; v[jt * 4 + 1] = a.y; v[jt * 4 + 2] = c.x; v[jt * 4 + 3] = c.y;
   }
+  u32x4 o;
+  if constexpr (sizeof(T) == 2) {
 #pragma unroll
-  for (int i = 0; i < 64; ++i) dst[i] = Elem<T>::from_f(v[i]);
+    for (int i = 0; i < 4; ++i) o[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = __float_as_uint(v[i]);
+  }
+  *(u32x4*)(col + (size_t)p * 64 + k * VEC) = o;
 }
 
 // ---- Philox4x32-10 -> Box-Muller complex normals -------------------------------------
@@ -263,7 +277,8 @@ extern "C" int snrse_input_pack(const void* x, const void* y, int B, int H, int 
                                 int dtype, hipStream_t s) {
   const int total = B * H * W;
   if (total <= 0) return SNRSE_EINVAL;
-  dim3 grid((total + 255) / 256);
+  const long long lanes = (long long)total * (dtype == SNRSE_BF16 ? 8 : 16);
+  dim3 grid((unsigned)((lanes + 255) / 256));
   if (dtype == SNRSE_BF16)
     hipLaunchKernelGGL(input_pack_kernel<bf16_t>, grid, dim3(256), 0, s, (const float2*)x, (const float2*)y, H, W,
                        (bf16_t*)col, pyr, total);

@@ -104,6 +104,7 @@ class NCSNppHIP:
             raise RuntimeError("snrse: NCSNppHIP needs a HIP device (no CPU fallback)")
         self.dtype = dtype
         self.device = torch.device(device)
+        self._arena = None  # ops.StatsArena of the GroupNorm statistics, one fill per evaluation
         self.plan = build_plan(**cfg)
         dev, dt = self.device, dtype
         f32 = lambda k: sd[k].detach().to(dev, torch.float32).contiguous()  # noqa: E731
@@ -231,6 +232,12 @@ class NCSNppHIP:
     def pyramid(self, x, y, t):
         """x, y complex64 [B,F,T] (contiguous, device); t [B] f32 -> final pyramid [B,F,T,4] f32
         (ncsnpp.py:389-398 before the division by t and the output layer)."""
+        if self._arena is None:
+            self._arena = ops.StatsArena(x.device)
+        with self._arena:
+            return self._pyramid(x, y, t)
+
+    def _pyramid(self, x, y, t):
         W = self.W
         dense = self.temb(t)
         col, pyr_in = ops.input_pack(x, y, self.dtype)

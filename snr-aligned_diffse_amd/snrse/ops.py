@@ -70,6 +70,7 @@ def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_w
     odt = torch.float32 if out_f32 else src0.dtype
     if out is None:
         out = torch.empty(B, H, W, cout, device=src0.device, dtype=odt)
+    _stats_zeroed(stats)
     _lib.call("snrse_conv2d", _ptr(src0), C0, _ptr(src1), C1, B, H, W, ksize, _ptr(wgt), _ptr(sc), Csc,
               _ptr(sc1), Csc1, _ptr(sc_wgt), _ptr(bias), None if temb is None else temb.data_ptr() + 4 * temb_off,
               0 if temb is None else temb.shape[1], _ptr(res), 0 if res is None else res.shape[-1], float(out_scale), _ptr(comb),
@@ -136,13 +137,70 @@ def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):
 STAT_SLOTS = 16  # SNRSE_STAT_SLOTS (include/snrse.h)
 
 
+_ARENA = []  # active StatsArena stack (innermost last)
+_ZEROED = {"v": 0}  # mirror of the library's "stats_zeroed" option
+
+
+class StatsArena:
+    """One f64 buffer per network evaluation, zeroed by a single fill, from which new_stats()
+    carves the GroupNorm statistics buffers; the producers are told (option "stats_zeroed") to
+    skip their per-call memset.  The first evaluation inside an arena only measures the size
+    (its buffers come from torch.empty and are cleared by the producers as usual)."""
+
+    ALIGN = 32  # doubles (256 B)
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.buf, self.off, self.need = None, 0, 0
+
+    def __enter__(self):
+        if self.buf is not None:
+            self.buf.zero_()
+        self.off, self.need = 0, 0
+        _ARENA.append(self)
+        return self
+
+    def __exit__(self, *exc):
+        _ARENA.remove(self)
+        if self.buf is None or self.need > self.buf.numel():
+            self.buf = torch.empty(self.need, dtype=torch.float64, device=self.device)
+        return False
+
+    def take(self, n):
+        na = (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        self.need += na
+        if self.buf is None or self.off + na > self.buf.numel():
+            return None
+        t = self.buf[self.off:self.off + n]
+        self.off += na
+        return t
+
+
+def _stats_zeroed(*bufs):
+    """Set the library's "stats_zeroed" option for a producer writing into `bufs`."""
+    bufs = [b for b in bufs if b is not None]
+    if not bufs:
+        return
+    z = int(all(getattr(b, "_snrse_zeroed", False) for b in bufs))
+    if _ZEROED["v"] != z:
+        _lib.call("snrse_set_option", b"stats_zeroed", z)
+        _ZEROED["v"] = z
+
+
 def new_stats(x_or_shape, C=None):
-    """Empty [B, STAT_SLOTS, C, 2] f64 per-channel statistics buffer for an NHWC tensor
-    (producers spread their atomics over the slots; consumers fold them)."""
+    """[B, STAT_SLOTS, C, 2] f64 per-channel statistics buffer for an NHWC tensor (producers
+    spread their atomics over the slots; consumers fold them).  Inside a StatsArena on the same
+    device the buffer is a pre-zeroed arena slice."""
     if C is None:
         B, C, dev = x_or_shape.shape[0], x_or_shape.shape[-1], x_or_shape.device
     else:
-        B, dev = x_or_shape, torch.device("cuda")
+        B, dev = x_or_shape, torch.device("cuda", torch.cuda.current_device())
+    if _ARENA and _ARENA[-1].device == torch.device(dev):
+        t = _ARENA[-1].take(B * STAT_SLOTS * C * 2)
+        if t is not None:
+            t = t.view(B, STAT_SLOTS, C, 2)
+            t._snrse_zeroed = True
+            return t
     return torch.empty(B, STAT_SLOTS, C, 2, device=dev, dtype=torch.float64)
 
 
@@ -158,6 +216,7 @@ def gn_stats(src0, src1=None):
     C1 = 0 if src1 is None else src1.shape[3]
     s0 = new_stats(src0)
     s1 = None if src1 is None else new_stats(src1)
+    _stats_zeroed(s0, s1)
     _lib.call("snrse_gn_stats", _ptr(src0), C0, _ptr(src1), C1, B, H * W, s0.data_ptr(), _ptr(s1),
               code(src0.dtype), _stream())
     return s0, s1

@@ -503,3 +503,25 @@ def test_conv_head_fused_groupnorm(gpu, shape):
     assert ops.kernel_name(ops.get_option("last_kernel")) == "conv_head_kernel"
     assert out.dtype == torch.float32
     assert rel(nchw(out), ref) < 1e-2
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_stats_arena_repeat_evaluations(gpu, sd_ncsnpp, dt):
+    """The first evaluation sizes the GroupNorm-statistics arena (per-producer memsets); later ones
+    carve pre-zeroed slices from it (option "stats_zeroed").  Both must match the golden output,
+    and the library option is left consistent with the buffers handed over."""
+    from snrse import ncsnpp, ops
+    g = golden("ncsnpp_full.npz")
+    net = ncsnpp.NCSNppHIP(sd_ncsnpp, dtype=DT[dt][0])
+    x = torch.from_numpy(fnormal("golden.ncsnpp.x", (2, 2, 256, 64), complex_=True)) * 0.5
+    t = torch.tensor([0.5, 0.8], device=gpu)
+    xg, yg = x[:, 0].contiguous().to(gpu), x[:, 1].contiguous().to(gpu)
+    outs = [net.dnn(xg, yg, t) for _ in range(3)]
+    assert net._arena.buf is not None and net._arena.need <= net._arena.buf.numel()
+    for o in outs:
+        assert rel(o, g["out"][:, 0]) < (1e-4 if dt == "f32" else 2e-2)
+    assert rel(outs[2], outs[1]) < (1e-6 if dt == "f32" else 1e-2)
+    # outside an arena the producers clear their own buffers again
+    s0, _ = ops.gn_stats(nhwc(torch.ones(2, 128, 8, 64, device=gpu, dtype=DT[dt][0])))
+    assert ops.get_option("stats_zeroed") == 0
+    assert torch.allclose(ops.fold_stats(s0)[..., 0], torch.full((2, 128), 512.0, device=gpu, dtype=torch.float64))
