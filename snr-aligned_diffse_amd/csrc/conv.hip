@@ -21,6 +21,8 @@
 // kernel needs because its fragments start at arbitrary (tap-shifted) rows.
 #include "conv_common.h"
 
+#include <type_traits>
+
 using namespace snrse_conv;
 
 namespace {
@@ -177,6 +179,20 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
   }
 }
 
+// Sum over the lanes of a wave that share lane % S (S = 8 or 16), every lane receives its sum:
+// DPP row rotate by 8 inside the 16-lane rows (S = 8), then row-pair and half-wave swaps
+// (v_permlane16_swap / v_permlane32_swap) -- VALU only, no ds_bpermute round trips.
+template <int S>
+SNRSE_DEV float sum_lanes_strided(float v) {
+  static_assert(S == 8 || S == 16, "lane stride");
+  if constexpr (S == 8)
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r2[0]) + __uint_as_float(r2[1]);
+}
+
 // Lean LDS-staged epilogue of the halo kernels: the wave's 64 rows are 64 consecutive pixels of
 // image `b` and its 64 channels are in range (H % 4 == 0, W % 64 == 0, Cout % 128 == 0 there), so
 // bias / temb / Combine weights are per-lane constants and no row or column masking is needed.
@@ -270,11 +286,8 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
   if (p.stats) {
 #pragma unroll
     for (int k = 0; k < EPC; ++k) {
-#pragma unroll
-      for (int o = NCH; o < 64; o <<= 1) {
-        s1[k] += __shfl_xor(s1[k], o, 64);
-        s2[k] += __shfl_xor(s2[k], o, 64);
-      }
+      s1[k] = sum_lanes_strided<NCH>(s1[k]);
+      s2[k] = sum_lanes_strided<NCH>(s2[k]);
     }
     if (r0 == 0) {
 #pragma unroll
@@ -1013,7 +1026,30 @@ int launch_halo(ConvParams p, hipStream_t s) {
 // prologue / epilogue runs under the other's MFMAs (v4 is 1 workgroup/CU, 152 KB).
 SNRSE_DEV int swz64(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >> 1) & 3)) << 4); }
 
-template <typename TO>
+SNRSE_DEV int h5_opaque(int v) {
+  int r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
+// per-CU arrival counter of the persistent v5 launches (key = XCC << 8 | HW_ID[15:8]); exactly two
+// workgroups per CU per launch keep each count's parity = arrival order
+__device__ unsigned g_h5_cu_arrivals[8 * 256];
+
+// GroupNorm prologue of the v5 halo kernel on one packed bf16 pair: GNM 1 = affine, 2 = affine + SiLU
+template <int GNM>
+SNRSE_DEV uint32_t gn_xform2(uint32_t v, float s0, float h0, float s1, float h1) {
+  float lo = __uint_as_float(v << 16), hi = __uint_as_float(v & 0xffff0000u);
+  lo = fmaf(lo, s0, h0);
+  hi = fmaf(hi, s1, h1);
+  if constexpr (GNM == 2) {
+    lo = silu(lo);
+    hi = silu(hi);
+  }
+  return pack_bf16x2(lo, hi);
+}
+
+template <typename TO, int GNM>
 __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   constexpr int TH = 4, TW = 64, HC = TW + 2;
   constexpr int HROWS = (TH + 2) * HC;  // 396
@@ -1035,7 +1071,37 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   SNRSE_STAMP(0);
   const int nb = gridDim.x, bid = blockIdx.x;
   const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7, pos = bid >> 3;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
+  const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
+  // persistent mode: workgroup g runs the contiguous tile range [t_begin, t_end) (consecutive g
+  // share an XCD, so an XCD walks neighbouring image rows).  The second workgroup to arrive on a
+  // CU starts p.h5_stagger ticks late, so the two co-resident workgroups' prologues / epilogues
+  // (HBM-latency and store bound) run under the other's MFMAs instead of in lockstep.
+  int t_begin = g, t_end = g + 1;
+  if (p.h5_tiles > 0) {
+    t_begin = (int)((long long)g * p.h5_tiles / nb);
+    t_end = (int)((long long)(g + 1) * p.h5_tiles / nb);
+    if (p.h5_stagger > 0) {
+      __shared__ unsigned h5_late;
+      if (tid == 0) {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        const unsigned key = ((xcc & 7u) << 8) | ((hw >> 8) & 0xffu);
+        h5_late = atomicAdd(&g_h5_cu_arrivals[key], 1u) & 1u;
+      }
+      __syncthreads();
+      if (h5_late) {
+        const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+        while (__builtin_amdgcn_s_memtime() - t_start < (unsigned long long)p.h5_stagger) __builtin_amdgcn_s_sleep(16);
+      }
+    }
+  }
+  for (int wg = t_begin; wg < t_end; ++wg) {
+  if (wg != t_begin) __syncthreads();  // LDS: the previous tile's epilogue staging is done
+  // lane-derived values are re-derived per tile from an opaque copy of the thread index, so the
+  // tile loop does not hoist them into VGPRs live across the whole tile (256-VGPR budget)
+  const int tid = h5_opaque((int)threadIdx.x), lane = tid & 63;
+  (void)lane;
   const int n0 = (wg % p.ntn) * 128;
   int tile = wg / p.ntn;
   const int ntw = p.W / TW, nth = p.H / TH;
@@ -1052,7 +1118,6 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   const int nq = 3 * cbm + cbs;
   const int K1 = 9 * Cin;
   const int hcol = tid & 3;  // this thread's 16-B chunk (8 channels) of its halo rows
-  const bool gn = p.gn_scale != nullptr;
 
   int hpix[HJ];
   bool hok[HJ];
@@ -1082,7 +1147,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
       const int ch = c * KT;
       if (ch < p.C0) SNRSE_HALO5_LOADS(p.src0, p.bytes0, p.C0, ch);
       else SNRSE_HALO5_LOADS(p.src1, p.bytes1, p.C1, ch - p.C0);
-      if (gn) {
+      if constexpr (GNM > 0) {
         const float* sp = p.gn_scale + (size_t)bb * Cin + ch + hcol * 8;
         const float* hp = p.gn_shift + (size_t)bb * Cin + ch + hcol * 8;
         const f32x4 s0 = *(const f32x4*)sp, s1 = *(const f32x4*)(sp + 4);
@@ -1098,24 +1163,19 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   };
 #undef SNRSE_HALO5_LOADS
   auto halo_store = [&](int c) {
-    const bool tr = gn && c < cbm;
+    const bool tr = GNM > 0 && c < cbm;
 #pragma unroll
     for (int j = 0; j < HJ; ++j) {
       const int hr = (tid >> 2) + 64 * j;
       if (j == HJ - 1 && hr >= HROWS) break;
       u32x4 v = hv[j];
-      if (tr) {
-        if (hok[j]) {
+      if constexpr (GNM > 0) {
+        if (tr) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float lo = __uint_as_float(v[i] << 16), hi = __uint_as_float(v[i] & 0xffff0000u);
-            lo = fmaf(lo, gsc[2 * i], gsh[2 * i]);
-            hi = fmaf(hi, gsc[2 * i + 1], gsh[2 * i + 1]);
-            if (p.gn_act) { lo = silu(lo); hi = silu(hi); }
-            v[i] = pack_bf16x2(lo, hi);
+            const uint32_t o = gn_xform2<GNM>(v[i], gsc[2 * i], gsh[2 * i], gsc[2 * i + 1], gsh[2 * i + 1]);
+            v[i] = hok[j] ? o : 0u;  // outside the image: the conv's zero padding
           }
-        } else {
-          v = u32x4{0u, 0u, 0u, 0u};
         }
       }
       *(u32x4*)(halo + swz64(hr, hcol)) = v;
@@ -1212,6 +1272,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   epilogue_img<TO, 4, 128, true>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0);
   SNRSE_STAMP(27);
   if (p.stats) block_stats_flush<4, 128>(p, red, bb, n0);
+  }  // tile loop
 #ifdef SNRSE_STAMPS
   {
     unsigned long long st_[29];
@@ -1233,8 +1294,13 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 #endif
 }
 
-template <typename TO>
-int launch_halo5(ConvParams p, hipStream_t s) {
+int g_h5_persist = 0;                 // option "h5_persist": persistent staggered v5 launches (measured
+                                      // 5-10 % slower than one tile per workgroup: off)
+int g_h5_slots = 512;                 // two workgroups per CU (256 CUs)
+int g_h5_stagger_per_phase = 3600;    // option "h5_stagger": s_memtime ticks per phase x nq / 2
+
+template <typename TO, int GNM>
+int launch_halo5_gn(ConvParams p, hipStream_t s) {
 #ifdef SNRSE_STAMPS
   constexpr size_t lds = 396 * 64 + 2 * 3 * 128 * 64 + 4 * 32 * 8;
 #else
@@ -1242,14 +1308,32 @@ int launch_halo5(ConvParams p, hipStream_t s) {
 #endif
   static bool attr = false;
   if (!attr) {
-    SNRSE_RET(hipFuncSetAttribute((const void*)conv_halo5_kernel<TO>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds));
+    SNRSE_RET(hipFuncSetAttribute((const void*)conv_halo5_kernel<TO, GNM>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
   p.ntn = p.Cout / 128;
-  const int tiles = p.B * (p.H / 4) * (p.W / 64);
-  hipLaunchKernelGGL((conv_halo5_kernel<TO>), dim3(tiles * p.ntn), dim3(256), lds, s, p);
+  const int tiles = p.B * (p.H / 4) * (p.W / 64) * p.ntn;
+  int grid = tiles;
+  p.h5_tiles = 0;
+  p.h5_stagger = 0;
+  if (g_h5_persist && tiles >= 4 * g_h5_slots) {  // >= 4 tiles per workgroup: stagger pays off
+    grid = g_h5_slots;
+    p.h5_tiles = tiles;
+    // ~half a tile: a 32-channel chunk of the 9-tap main loop takes ~1.7e3 ticks per phase
+    const int nq = 3 * ((p.C0 + p.C1) / 32) + (p.sc_src ? (p.Csc + p.Csc1) / 32 : 0);
+    p.h5_stagger = g_h5_stagger_per_phase * nq / 2;
+  }
+  hipLaunchKernelGGL((conv_halo5_kernel<TO, GNM>), dim3(grid), dim3(256), lds, s, p);
   return (int)hipGetLastError();
+}
+
+// GroupNorm prologue mode as a template argument: the halo transform is straight-line code
+template <typename TO>
+int launch_halo5(ConvParams p, hipStream_t s) {
+  if (!p.gn_scale) return launch_halo5_gn<TO, 0>(p, s);
+  if (!p.gn_act) return launch_halo5_gn<TO, 1>(p, s);
+  return launch_halo5_gn<TO, 2>(p, s);
 }
 
 template <typename T, typename TO, int BM, int BN, int WM, int WN>
@@ -1433,6 +1517,8 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   }
   if (name_is(name, "last_kernel")) { *value = g_last_kernel; return 0; }
   if (name_is(name, "splitk")) { *value = g_splitk; return 0; }
+  if (name_is(name, "h5_persist")) { *value = g_h5_persist; return 0; }
+  if (name_is(name, "h5_stagger")) { *value = g_h5_stagger_per_phase; return 0; }
   if (name_is(name, "stats_zeroed")) { *value = g_snrse_stats_zeroed; return 0; }
   if (name_is(name, "last_ksplit")) { *value = g_last_ksplit; return 0; }
   return SNRSE_EINVAL;
@@ -1442,6 +1528,8 @@ extern "C" int snrse_set_option(const char* name, int value) {
   if (!name) return SNRSE_EINVAL;
   if (name_is(name, "conv_variant")) { g_conv_variant = value; return 0; }
   if (name_is(name, "splitk")) { g_splitk = value; return 0; }
+  if (name_is(name, "h5_persist")) { g_h5_persist = value; return 0; }
+  if (name_is(name, "h5_stagger")) { g_h5_stagger_per_phase = value; return 0; }
   if (name_is(name, "stats_zeroed")) { g_snrse_stats_zeroed = value ? 1 : 0; return 0; }
   return SNRSE_EINVAL;
 }

@@ -42,6 +42,8 @@ struct ConvParams {
   float* ws;              // split-K partial sums [ksplit][M][Cout] f32 (caller-registered workspace)
   int ksplit;             // K splits of the v2 GEMM (1: the epilogue runs in the GEMM itself)
   unsigned long long* stamps;  // timing-diagnostic build only (-DSNRSE_STAMPS): [blocks][8][32]
+  int h5_tiles;    // v5 persistent mode: total output tiles (0 = one tile per workgroup)
+  int h5_stagger;  // v5: s_memtime ticks the second workgroup of a CU waits before its first tile
 };
 
 #ifdef SNRSE_STAMPS
