@@ -179,7 +179,28 @@ class ScoreModel(nn.Module):
         return batched_sampling_fn
 
     def get_ode_sampler(self, y, Y_prior=None, N=None, minibatch=None, timestep_type=None, **kwargs):
-        return sampling.get_ode_sampler(self.sde, self, y)
+        """model.py:574-595.  As in the reference, the minibatched variant returns the LAST
+        minibatch's sample (`return sample, ns`, model.py:594) -- kept for drop-in behaviour."""
+        N = self.sde.N if N is None else N
+        sde = self.sde.copy()
+        sde.N = N
+        kwargs = {"eps": self.t_eps, **kwargs}
+        if minibatch is None:
+            return sampling.get_ode_sampler(sde, self, y=y, Y_prior=Y_prior, timestep_type=timestep_type, **kwargs)
+        M = y.shape[0]
+
+        def batched_sampling_fn():
+            samples, ns = [], []
+            sample = None
+            for i in range(int(ceil(M / minibatch))):
+                y_mini = y[i * minibatch:(i + 1) * minibatch]
+                sampler = sampling.get_ode_sampler(sde, self, y=y_mini, **kwargs)
+                sample, n = sampler()
+                samples.append(sample)
+                ns.append(n)
+            return sample, ns
+
+        return batched_sampling_fn
 
     # ------------------------------------------------------------------ spectrogram glue
     def to_audio(self, spec, length=None):

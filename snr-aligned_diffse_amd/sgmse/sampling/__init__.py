@@ -64,7 +64,44 @@ def get_pc_sampler(predictor_name, corrector_name, sde, score_fn, Y, Y_prior=Non
     return pc_sampler
 
 
-def get_ode_sampler(sde, score_fn, y, *args, **kwargs):
-    """Probability-flow ODE sampler (scipy RK45, sampling/__init__.py:95-171): listed as a
-    'next' item, not part of the HIP build yet."""
-    raise NotImplementedError("the ODE sampler is not part of the MI355X build yet (SURVEY.md §8(f) item 4)")
+def get_ode_sampler(sde, score_fn, y, Y_prior=None, inverse_scaler=None, denoise=True, rtol=1e-5, atol=1e-5,
+                    timestep_type=None, method="RK45", eps=3e-2, device="cuda", **kwargs):
+    """Probability-flow ODE sampler (sampling/__init__.py:95-171): prior sample at T, integrate
+    dx/dt = f(x, t, y) - 1/2 g(t)^2 score(x, t, y) from T down to eps with adaptive RK45, then
+    (denoise) one noise-free ReverseDiffusion step at eps with stepsize 0.03.  Returns
+    (x complex64 shaped like y, nfev).  The integrator is `snrse.ode.rk45_solve` -- scipy's RK45
+    restated on the device state (no host round trip of the spectrogram per evaluation); the
+    score is whatever `score_fn` runs (the HIP NCSN++ for a ScoreModel).  Extra kwargs are
+    accepted and ignored (scipy warns about them and ignores them too)."""
+    from snrse.ode import rk45_solve
+
+    if method != "RK45":
+        raise NotImplementedError(f"ODE method {method!r}: only RK45 (the reference default) is built")
+    predictor = ReverseDiffusionPredictor(sde, score_fn, probability_flow=False)
+    rsde = sde.reverse(score_fn, probability_flow=True)
+    T = float(sde.T)
+
+    def ode_sampler(z=None, Y_prior=Y_prior, **kw):
+        with torch.no_grad():
+            yp = y if Y_prior is None else Y_prior
+            if not y.is_cuda:
+                raise RuntimeError("ode_sampler: HIP device tensors required (no CPU fallback)")
+            xt, _ = sde.prior_sampling(yp.shape, yp)
+            x0 = xt.to(yp.device)
+            B = y.shape[0]
+
+            def drift(t, xs):
+                xc = xs.reshape(y.shape).to(torch.complex64)
+                vec_t = torch.ones(B, device=xc.device) * t
+                return rsde.sde(xc, vec_t, y)[0]
+
+            res = rk45_solve(drift, T, eps, x0, rtol=rtol, atol=atol)
+            x = res.y.reshape(y.shape).to(torch.complex64)
+            if denoise:
+                vec_eps = torch.ones(B, device=x.device) * eps
+                _, x = predictor.update_fn(x, vec_eps, y, 0.03)
+            if inverse_scaler is not None:
+                x = inverse_scaler(x)
+            return x, res.nfev
+
+    return ode_sampler
