@@ -98,3 +98,24 @@ def pad_spec(Y, mult=64):
     n = (mult - T % mult) if T % mult else 0
     pad = [(0, 0)] * (Y.ndim - 1) + [(0, n)]
     return np.pad(Y, pad)
+
+
+def specs_item(x: np.ndarray, y: np.ndarray, num_frames: int = 256, normalize: str = "noisy", fixed_snr: float = 1.0,
+               start: int | None = None):
+    """Specs.__getitem__ (data_module.py:47-84) on decoded mono clips x, y [L]: mix, crop at
+    `start` (the centred start when None) or zero-pad (pad//2 left), normalise, STFT, spec_fwd.
+    -> (X, Y) complex [256, num_frames]."""
+    x = np.asarray(x, np.float64)
+    y = np.asarray(y, np.float64)
+    y = x + (y - x) * fixed_snr
+    target = (num_frames - 1) * HOP
+    cur = x.shape[-1]
+    pad = max(target - cur, 0)
+    if pad == 0:
+        s = int((cur - target) / 2) if start is None else start
+        x, y = x[s:s + target], y[s:s + target]
+    else:
+        x = np.pad(x, (pad // 2, pad // 2 + pad % 2))
+        y = np.pad(y, (pad // 2, pad // 2 + pad % 2))
+    nf = {"noisy": np.abs(y).max(), "clean": np.abs(x).max(), "not": 1.0}[normalize]
+    return spec_fwd(stft((x / nf)[None])[0]), spec_fwd(stft((y / nf)[None])[0])

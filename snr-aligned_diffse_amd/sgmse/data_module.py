@@ -1,14 +1,24 @@
 """SpecsDataModule — the spectrogram front/back end of the reference (data_module.py:178-297),
 importable without pytorch_lightning / torchaudio (checkpoints unpickle it by qualified name,
 model.py:45,93).  stft / istft / spec_fwd / spec_back run on the HIP kernels for device
-tensors (n_fft 510, hop 128, periodic Hann, center=True, the 'exponent' transform); the
-dataset / DataLoader half of the reference is training-side and out of scope.
+tensors (n_fft 510, hop 128, periodic Hann, center=True, the 'exponent' transform).
+
+Front-end: `Specs` / `Specs_SNR` (data_module.py:22-176) read the clean /
+noisy WAV pairs (snrse.audio, torchaudio.load semantics), crop or zero-pad to num_frames on the
+host (the only per-clip host work: index arithmetic on the decoded samples) and run the
+mix / normalisation / STFT / spectrogram transform as device kernels.  `Specs.batch(indices)`
+does that for a whole batch in one upload, one absmax, one fused STFT+transform launch per
+signal, so batches reach the sampler at device speed.
 """
 from __future__ import annotations
 
+from glob import glob
+from os.path import join
+
+import numpy as np
 import torch
 
-from snrse import ops
+from snrse import audio, ops
 
 
 def get_window(window_type, window_length):
@@ -17,6 +27,125 @@ def get_window(window_type, window_length):
     if window_type == "hann":
         return torch.hann_window(window_length, periodic=True)
     raise NotImplementedError(f"Window type {window_type} not implemented!")
+
+
+def _device():
+    if not torch.cuda.is_available():
+        raise RuntimeError("Specs: the front-end runs on the HIP device (no CPU fallback)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class Specs(torch.utils.data.Dataset):
+    """Clean/noisy pairs -> (X, Y) complex64 [1, 256, num_frames] on the device
+    (data_module.py:22-90): y = x + (y - x) fixed_snr; crop (random start when shuffle_spec,
+    centred otherwise) or zero-pad (pad//2 left) to (num_frames - 1) hop samples; divide by
+    max|y| ('noisy'), max|x| ('clean') or 1 ('not'); STFT; spec_transform."""
+
+    def __init__(self, data_dir, subset, dummy, shuffle_spec, num_frames, format="default", normalize="noisy",
+                 spec_transform=None, stft_kwargs=None, fixed_snr=1, **ignored_kwargs):
+        if format != "default":
+            raise NotImplementedError(f"Directory format {format} unknown!")
+        self.clean_files = sorted(glob(join(data_dir, subset) + "/clean/*.wav"))
+        self.noisy_files = sorted(glob(join(data_dir, subset) + "/noisy/*.wav"))
+        self.dummy, self.num_frames, self.shuffle_spec = dummy, num_frames, shuffle_spec
+        self.normalize, self.spec_transform, self.fixed_snr = normalize, spec_transform, fixed_snr
+        stft_kwargs = stft_kwargs or dict(n_fft=510, hop_length=128, center=True, window=get_window("hann", 510))
+        assert all(k in stft_kwargs.keys() for k in ["n_fft", "hop_length", "center", "window"]), \
+            "misconfigured STFT kwargs"
+        self.stft_kwargs = stft_kwargs
+        self.hop_length = stft_kwargs["hop_length"]
+        assert stft_kwargs.get("center", None) is True, "'center' must be True for current implementation"
+        if (stft_kwargs["n_fft"], self.hop_length) != (510, 128):
+            raise NotImplementedError("the HIP STFT is built for n_fft=510, hop 128")
+
+    def _crop(self, x, y):
+        """Host crop / pad of one [C, L] pair (data_module.py:53-68)."""
+        target_len = (self.num_frames - 1) * self.hop_length
+        cur = x.shape[-1]
+        pad = max(target_len - cur, 0)
+        if pad == 0:
+            start = int(np.random.uniform(0, cur - target_len)) if self.shuffle_spec else int((cur - target_len) / 2)
+            return x[..., start:start + target_len], y[..., start:start + target_len]
+        pw = (pad // 2, pad // 2 + (pad % 2))
+        return (torch.nn.functional.pad(x, pw, mode="constant"), torch.nn.functional.pad(y, pw, mode="constant"))
+
+    def _load_pair(self, i):
+        x, _ = audio.load(self.clean_files[i])
+        y, _ = audio.load(self.noisy_files[i])
+        return x, y
+
+    def _specs(self, xs, ys, fixed_snr):
+        """Device half for stacked host crops xs, ys [B, L] -> (X, Y) [B, 1, 256, num_frames]."""
+        dev = _device()
+        B = xs.shape[0]
+        xy = torch.cat([xs, ys], 0).to(dev, torch.float32, non_blocking=True)
+        x, y = xy[:B], xy[B:]
+        if fixed_snr != 1:
+            y = (x + (y - x) * fixed_snr).contiguous()
+        if self.normalize == "noisy":
+            nf = ops.absmax(y)
+        elif self.normalize == "clean":
+            nf = ops.absmax(x)
+        elif self.normalize == "not":
+            nf = None
+        else:
+            raise ValueError(f"normalize {self.normalize!r}")
+        fused = getattr(self.spec_transform, "__func__", None) is SpecsDataModule.spec_fwd and \
+            self.spec_transform.__self__.transform_type == "exponent"
+        mode = 1 if fused else 0
+        X = ops.stft(x.contiguous(), 1.0, mode=mode, in_div=nf)
+        Y = ops.stft(y.contiguous(), 1.0, mode=mode, in_div=nf)
+        if not fused and self.spec_transform is not None:
+            X, Y = self.spec_transform(X), self.spec_transform(Y)
+        return X[:, None], Y[:, None]
+
+    def __getitem__(self, i):
+        x, y = self._load_pair(i)
+        x, y = self._crop(x, y)
+        X, Y = self._specs(x, y, self.fixed_snr)
+        return X[0], Y[0]
+
+    def batch(self, indices):
+        """(X, Y) [len(indices), 1, 256, num_frames] for a list of clip indices, one device pass
+        (mono clips; the per-item path handles [C, L] like the reference)."""
+        xs, ys = [], []
+        for i in indices:
+            x, y = self._crop(*self._load_pair(i))
+            if x.shape[0] != 1:
+                raise ValueError("Specs.batch: mono clips only")
+            xs.append(x[0])
+            ys.append(y[0])
+        return self._specs(torch.stack(xs), torch.stack(ys), self.fixed_snr)
+
+    def __len__(self):
+        return int(len(self.clean_files) / 200) if self.dummy else len(self.clean_files)
+
+
+class Specs_SNR(Specs):
+    """Validation set with per-clip active RMS (data_module.py:93-176): items are (X, Y, s, n)
+    with s, n the clean / noise active RMS read from <subset>/active_rms.txt (tab-separated,
+    columns 1 and 2); no fixed_snr mixing.  (The reference's __len__ returns None unless dummy;
+    here it is the clip count.)"""
+
+    def __init__(self, data_dir, subset, dummy, shuffle_spec, num_frames, format="default", normalize="noisy",
+                 spec_transform=None, stft_kwargs=None, **ignored_kwargs):
+        super().__init__(data_dir, subset, dummy, shuffle_spec, num_frames, format=format, normalize=normalize,
+                         spec_transform=spec_transform, stft_kwargs=stft_kwargs, fixed_snr=1)
+        self.active_rms = join(data_dir, subset) + "/active_rms.txt"
+        self.clean_rms, self.noise_rms = [], []
+        with open(self.active_rms, "r") as f:
+            for line in f:
+                parts = line.split("\t")
+                try:
+                    s_, n_ = float(parts[1]), float(parts[2])
+                except (IndexError, ValueError):
+                    break  # the reference stops at the first malformed line
+                self.clean_rms.append(s_)
+                self.noise_rms.append(n_)
+
+    def __getitem__(self, i):
+        X, Y = super().__getitem__(i)
+        return X, Y, self.clean_rms[i], self.noise_rms[i]
 
 
 class SpecsDataModule:
@@ -59,7 +188,36 @@ class SpecsDataModule:
             raise NotImplementedError(f"transform_type {self.transform_type} is not built for the HIP path")
 
     def setup(self, stage=None):
-        raise NotImplementedError("training datasets are out of scope of the inference build")
+        """Datasets of data_module.py:221-240 (device-producing Specs / Specs_SNR)."""
+        self._check()
+        kw = dict(stft_kwargs=self.istft_kwargs, num_frames=self.num_frames, spec_transform=self.spec_fwd,
+                  **self.kwargs)
+        if stage == "fit" or stage is None:
+            self.train_set = Specs(data_dir=self.base_dir, subset="train", dummy=self.dummy, shuffle_spec=True,
+                                   format=self.format, normalize=self.normalize, fixed_snr=self.fixed_snr, **kw)
+            self.valid_set = Specs_SNR(data_dir=self.base_dir, subset="valid", dummy=self.dummy, shuffle_spec=False,
+                                       format=self.format, normalize=self.normalize, **kw)
+            self.valid_set_2 = Specs(data_dir=self.base_dir, subset="valid2", dummy=self.dummy, shuffle_spec=False,
+                                     fixed_snr=1, format=self.format, normalize=self.normalize, **kw)
+        if stage == "test" or stage is None:
+            self.test_set = Specs(data_dir=self.base_dir, subset="test", dummy=self.dummy, shuffle_spec=False,
+                                  format=self.format, normalize=self.normalize, fixed_snr=1, **kw)
+
+    # DataLoaders of data_module.py:299-321; items are device tensors, so loading stays in-process
+    def _loader(self, ds, batch_size, shuffle):
+        return torch.utils.data.DataLoader(ds, batch_size=batch_size, num_workers=0, shuffle=shuffle, drop_last=True)
+
+    def train_dataloader(self):
+        return self._loader(self.train_set, self.batch_size, True)
+
+    def val_dataloader(self):
+        return self._loader(self.valid_set, 1, False)
+
+    def val_dataloader_2(self):
+        return self._loader(self.valid_set_2, self.batch_size, False)
+
+    def test_dataloader(self):
+        return self._loader(self.test_set, self.batch_size, False)
 
     @property
     def stft_kwargs(self):
