@@ -156,6 +156,12 @@ int snrse_sde_update(const void* x, const void* y, const void* score, const void
 int snrse_axpby_noise(const void* x, const void* y, const void* noise, uint64_t seed, uint64_t offset,
                       const float* coef, int B, int HW, void* out, hipStream_t stream);
 
+/* Evaluation metrics (eval.py:144-157 -> utils.py:10-35 energy_ratios, sgmse/util/other.py:71-75
+ * si_sdr), batched: s_hat, s, n [B][L] f32 (n may be NULL) -> out [B][3] f64 = (SI-SDR, SI-SIR,
+ * SI-SAR) in dB from six fp64 dot products per utterance; SI-SIR / SI-SAR are NaN without n. */
+int snrse_energy_ratios(const float* s_hat, const float* s, const float* n, int B, int L, double* out,
+                        hipStream_t stream);
+
 /* norm_factor = max |y| per utterance (model.py:726): out[b] = max_i |sig[b][i]|. */
 int snrse_absmax(const float* sig, int B, int L, float* out, hipStream_t stream);
 

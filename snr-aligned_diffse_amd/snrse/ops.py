@@ -366,6 +366,20 @@ def axpby_noise(coef, x=None, y=None, noise=None, seed=0, offset=0, like=None):
     return out
 
 
+def energy_ratios(s_hat, s, n=None):
+    """[B, L] f32 device waveforms -> [B, 3] f64 (SI-SDR, SI-SIR, SI-SAR) dB (utils.py:10-35);
+    without n only SI-SDR (column 0) is defined (sgmse/util/other.py:71-75)."""
+    B, L = s_hat.shape
+    if s.shape != s_hat.shape or (n is not None and n.shape != s_hat.shape):
+        raise ValueError("energy_ratios: s_hat, s, n must share one [B, L] shape")
+    a = [t.to(torch.float32).contiguous() for t in (s_hat, s)]
+    nn = None if n is None else n.to(torch.float32).contiguous()
+    _dev(a[0], a[1], nn)
+    out = torch.empty(B, 3, device=s_hat.device, dtype=torch.float64)
+    _lib.call("snrse_energy_ratios", a[0].data_ptr(), a[1].data_ptr(), _ptr(nn), B, L, out.data_ptr(), _stream())
+    return out
+
+
 def absmax(sig):
     """[B, L] f32 -> [B] max |sig| per row."""
     _dev(sig)
