@@ -277,7 +277,10 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] = __float_as_uint(v[k]);
     }
-    *(u32x4*)((TO*)p.out + m * p.out_ld + n) = o;
+    if (p.epi_nt)  // option "epi_nt": streaming (non-temporal) output stores
+      __builtin_nontemporal_store(o, (u32x4*)((TO*)p.out + m * p.out_ld + n));
+    else
+      *(u32x4*)((TO*)p.out + m * p.out_ld + n) = o;
     if (p.stats) {
 #pragma unroll
       for (int k = 0; k < EPC; ++k) { s1[k] += v[k]; s2[k] = fmaf(v[k], v[k], s2[k]); }
@@ -1294,6 +1297,9 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 #endif
 }
 
+int g_epi_nt = 2;                     // option "epi_nt": non-temporal epilogue stores of the v5 halo GEMM:
+                                      // 0 off, 1 on, 2 when the output exceeds the 256 MB Infinity
+                                      // Cache (+1 % on the full-resolution convs, tools/h5_sweep.py)
 int g_h5_persist = 0;                 // option "h5_persist": persistent staggered v5 launches (measured
                                       // 5-10 % slower than one tile per workgroup: off)
 int g_h5_slots = 512;                 // two workgroups per CU (256 CUs)
@@ -1313,6 +1319,7 @@ int launch_halo5_gn(ConvParams p, hipStream_t s) {
     attr = true;
   }
   p.ntn = p.Cout / 128;
+  p.epi_nt = g_epi_nt == 2 ? ((long long)p.M * p.out_ld * (long long)sizeof(TO) > (256ll << 20)) : g_epi_nt;
   const int tiles = p.B * (p.H / 4) * (p.W / 64) * p.ntn;
   int grid = tiles;
   p.h5_tiles = 0;
@@ -1474,6 +1481,7 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
   p.comb_src = comb_src; p.comb_w = comb_w; p.comb_b = comb_b;
   p.out = out; p.Cout = Cout; p.out_ld = out_ld; p.M = B * H * W;
   p.stats = stats;
+  p.epi_nt = 0;
   p.ws = nullptr; p.ksplit = 1;
   p.gn_scale = gn_scale; p.gn_shift = gn_shift; p.gn_act = gn_act;
   if ((gn_scale == nullptr) != (gn_shift == nullptr)) return SNRSE_EINVAL;
@@ -1518,6 +1526,7 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   if (name_is(name, "last_kernel")) { *value = g_last_kernel; return 0; }
   if (name_is(name, "splitk")) { *value = g_splitk; return 0; }
   if (name_is(name, "h5_persist")) { *value = g_h5_persist; return 0; }
+  if (name_is(name, "epi_nt")) { *value = g_epi_nt; return 0; }
   if (name_is(name, "h5_stagger")) { *value = g_h5_stagger_per_phase; return 0; }
   if (name_is(name, "stats_zeroed")) { *value = g_snrse_stats_zeroed; return 0; }
   if (name_is(name, "last_ksplit")) { *value = g_last_ksplit; return 0; }
@@ -1529,6 +1538,7 @@ extern "C" int snrse_set_option(const char* name, int value) {
   if (name_is(name, "conv_variant")) { g_conv_variant = value; return 0; }
   if (name_is(name, "splitk")) { g_splitk = value; return 0; }
   if (name_is(name, "h5_persist")) { g_h5_persist = value; return 0; }
+  if (name_is(name, "epi_nt")) { g_epi_nt = value; return 0; }
   if (name_is(name, "h5_stagger")) { g_h5_stagger_per_phase = value; return 0; }
   if (name_is(name, "stats_zeroed")) { g_snrse_stats_zeroed = value ? 1 : 0; return 0; }
   return SNRSE_EINVAL;

@@ -44,6 +44,7 @@ struct ConvParams {
   unsigned long long* stamps;  // timing-diagnostic build only (-DSNRSE_STAMPS): [blocks][8][32]
   int h5_tiles;    // v5 persistent mode: total output tiles (0 = one tile per workgroup)
   int h5_stagger;  // v5: s_memtime ticks the second workgroup of a CU waits before its first tile
+  int epi_nt;      // image-tile epilogue: non-temporal output stores
 };
 
 #ifdef SNRSE_STAMPS

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Sweep of the persistent / staggered v5 halo-GEMM launch options on the conv_bench shapes.
 Usage (GPU box): python tools/h5_sweep.py [--gn] [--shapes 0,3] [--settings "0:0,1:0,1:3600"]
-(setting = h5_persist:h5_stagger).  Outputs of every setting are compared with the first one."""
+(setting = h5_persist:h5_stagger[:epi_nt]).  Outputs of every setting are compared with the first one."""
 import argparse
 import json
 import os
@@ -31,11 +31,13 @@ def main():
         row = {"shape": sh, "gn": a.gn}
         ref = None
         for rnd in range(2):
-            for pers, stg in sets:
+            for st in sets:
+                pers, stg, nt = (list(st) + [0])[:3]
                 ops.set_option("h5_persist", pers)
                 ops.set_option("h5_stagger", stg)
+                ops.set_option("epi_nt", nt)
                 out, ms, fl = run(sh, 5, a.reps, dev, gn=a.gn)
-                key = f"p{pers}_s{stg}"
+                key = f"p{pers}_s{stg}_nt{nt}"
                 row[key] = round(min(ms, row.get(key, ms)) * 1e3, 1)
                 row[key + "_tf"] = round(fl / (row[key] * 1e-3) / 1e9, 1)
                 if ref is None:
@@ -43,8 +45,9 @@ def main():
                 else:
                     row["maxdiff"] = max(row.get("maxdiff", 0.0), (out.float() - ref).abs().max().item())
         print(json.dumps(row), flush=True)
-    ops.set_option("h5_persist", 1)
+    ops.set_option("h5_persist", 0)
     ops.set_option("h5_stagger", 3600)
+    ops.set_option("epi_nt", 0)
 
 
 if __name__ == "__main__":
