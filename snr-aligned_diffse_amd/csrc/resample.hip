@@ -79,36 +79,53 @@ __global__ __launch_bounds__(256) void gn_resample_kernel(const bf16_t* __restri
   const int c0 = cg * kCB;
   const int tid = threadIdx.x;
 
-  // stage: raw bf16 + act(x * scale + shift) f32; outside the image both are zero (zero padding)
-  for (int idx = tid; idx < NPX * kNV; idx += 256) {
-    const int v = idx % kNV, p = idx / kNV;
+  // stage: raw bf16 + act(x * scale + shift) f32; outside the image both are zero (zero padding).
+  // Every thread keeps one 8-channel half of the group (v = tid & 1, since 256 % kNV == 0), so its
+  // scale / shift are loaded once, and all of its input vectors are issued before the first use
+  // (NIT loads in flight per thread instead of one).
+  static_assert(256 % kNV == 0, "channel half per thread");
+  constexpr int NIT = (NPX * kNV + 255) / 256;
+  const int v = tid % kNV;
+  const int c = c0 + 8 * v;
+  float sc[8], sh[8];
+  if (scale) {
+    const float* sp = scale + (size_t)b * C + c;
+    const float* hp = shift + (size_t)b * C + c;
+    const f32x4 s0 = *(const f32x4*)sp, s1 = *(const f32x4*)(sp + 4);
+    const f32x4 h0 = *(const f32x4*)hp, h1 = *(const f32x4*)(hp + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      sc[i] = s0[i]; sc[i + 4] = s1[i];
+      sh[i] = h0[i]; sh[i + 4] = h1[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { sc[i] = 1.f; sh[i] = 0.f; }
+  }
+  u32x4 rv[NIT];
+  bool inb[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = tid + 256 * k;
+    const int p = idx / kNV;
     const int ly = p / T::ITX, lx = p - ly * T::ITX;
     const int iy = iy0 + ly, ix = ix0 + lx;
-    u32x4 r = {0u, 0u, 0u, 0u};
-    float a[8];
-    const int c = c0 + 8 * v;
-    if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-      r = *(const u32x4*)(src + (((size_t)b * H + iy) * W + ix) * C + c);
-      float x[8];
-      unpack8(r, x);
-      if (scale) {
-        const float* sp = scale + (size_t)b * C + c;
-        const float* hp = shift + (size_t)b * C + c;
-        const f32x4 s0 = *(const f32x4*)sp, s1 = *(const f32x4*)(sp + 4);
-        const f32x4 h0 = *(const f32x4*)hp, h1 = *(const f32x4*)(hp + 4);
+    inb[k] = idx < NPX * kNV && iy >= 0 && iy < H && ix >= 0 && ix < W;
+    rv[k] = inb[k] ? *(const u32x4*)(src + (((size_t)b * H + iy) * W + ix) * C + c) : u32x4{0u, 0u, 0u, 0u};
+  }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          x[i] = fmaf(x[i], s0[i], h0[i]);
-          x[i + 4] = fmaf(x[i + 4], s1[i], h1[i]);
-        }
-      }
+  for (int k = 0; k < NIT; ++k) {
+    const int idx = tid + 256 * k;
+    if (idx >= NPX * kNV) break;
+    const int p = idx / kNV;
+    float x[8], a[8];
+    unpack8(rv[k], x);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = act ? silu(x[i]) : x[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = 0.f;
+    for (int i = 0; i < 8; ++i) {
+      const float y = fmaf(x[i], sc[i], sh[i]);
+      a[i] = inb[k] ? (act ? silu(y) : y) : 0.f;
     }
-    *(u32x4*)(s_raw + p * kCB + 8 * v) = r;
+    *(u32x4*)(s_raw + p * kCB + 8 * v) = rv[k];
     f32x4* d = (f32x4*)(s_act + p * kCB + 8 * v);
     d[0] = f32x4{a[0], a[1], a[2], a[3]};
     d[1] = f32x4{a[4], a[5], a[6], a[7]};
@@ -117,7 +134,7 @@ __global__ __launch_bounds__(256) void gn_resample_kernel(const bf16_t* __restri
 
   constexpr int NOUT = T::OTY * T::OTX * kNV;
   for (int idx = tid; idx < NOUT; idx += 256) {
-    const int v = idx % kNV, p = idx / kNV;
+    const int p = idx / kNV;  // idx % kNV == v: the thread's channel half, as in the staging
     const int ly = p / T::OTX, lx = p - ly * T::OTX;
     const int oy = oy0 + ly, ox = ox0 + lx;
     if (oy >= Ho || ox >= Wo) continue;
