@@ -10,8 +10,10 @@
 // One pass reads x once, activates every input pixel once (the per-output gn_apply kernel
 // re-activated each input 4x (down) / 16x (up) and folded the statistics in every block), and
 // writes both the activated and the raw resampled tensors; the block's input tile is staged in
-// LDS as f32 (activated) + bf16 (raw).
+// LDS (raw bf16; activated bf16 for down, f32 for up; f32 FIR arithmetic).
 #include "common.h"
+
+#include <type_traits>
 
 namespace {
 
@@ -63,7 +65,11 @@ __global__ __launch_bounds__(256) void gn_resample_kernel(const bf16_t* __restri
                                                           bf16_t* __restrict__ out_act, bf16_t* __restrict__ out_raw) {
   using T = RTile<MODE>;
   constexpr int NPX = T::ITY * T::ITX;
-  __shared__ __attribute__((aligned(16))) float s_act[NPX * kCB];
+  // down: the activated tile is kept as bf16 (2 x 19.6 KB instead of 39 + 19.6 KB, so 4 blocks
+  // share a CU: level-0 759 -> 501 us); up (17 KB tile, 4 taps per output) keeps f32, where the
+  // extra unpacking cost more than the occupancy gained
+  using ActT = std::conditional_t<MODE == MODE_DOWN, bf16_t, float>;
+  __shared__ __attribute__((aligned(16))) ActT s_act[NPX * kCB];
   __shared__ __attribute__((aligned(16))) bf16_t s_raw[NPX * kCB];
   const int ncg = C / kCB;
   int id = xcd_logical(blockIdx.x, gridDim.x);
@@ -126,9 +132,13 @@ __global__ __launch_bounds__(256) void gn_resample_kernel(const bf16_t* __restri
       a[i] = inb[k] ? (act ? silu(y) : y) : 0.f;
     }
     *(u32x4*)(s_raw + p * kCB + 8 * v) = rv[k];
-    f32x4* d = (f32x4*)(s_act + p * kCB + 8 * v);
-    d[0] = f32x4{a[0], a[1], a[2], a[3]};
-    d[1] = f32x4{a[4], a[5], a[6], a[7]};
+    if constexpr (MODE == MODE_DOWN) {
+      *(u32x4*)(s_act + p * kCB + 8 * v) = pack8(a);
+    } else {
+      f32x4* d = (f32x4*)(s_act + p * kCB + 8 * v);
+      d[0] = f32x4{a[0], a[1], a[2], a[3]};
+      d[1] = f32x4{a[4], a[5], a[6], a[7]};
+    }
   }
   __syncthreads();
 
@@ -146,14 +156,17 @@ __global__ __launch_bounds__(256) void gn_resample_kernel(const bf16_t* __restri
     }
     auto tap = [&](int py, int px, float w) {
       const int q = (py * T::ITX + px) * kCB + 8 * v;
-      const f32x4 a0 = *(const f32x4*)(s_act + q), a1 = *(const f32x4*)(s_act + q + 4);
-      float x[8];
+      float x[8], ac[8];
+      if constexpr (MODE == MODE_DOWN) {
+        unpack8(*(const u32x4*)(s_act + q), ac);
+      } else {
+        const f32x4 a0 = *(const f32x4*)(s_act + q), a1 = *(const f32x4*)(s_act + q + 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { ac[i] = a0[i]; ac[i + 4] = a1[i]; }
+      }
       unpack8(*(const u32x4*)(s_raw + q), x);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        oa[i] = fmaf(a0[i], w, oa[i]);
-        oa[i + 4] = fmaf(a1[i], w, oa[i + 4]);
-      }
+      for (int i = 0; i < 8; ++i) oa[i] = fmaf(ac[i], w, oa[i]);
 #pragma unroll
       for (int i = 0; i < 8; ++i) orw[i] = fmaf(x[i], w, orw[i]);
     };
