@@ -130,6 +130,14 @@ int snrse_temb_mlp(const float* t, const float* Wg, const float* W1, const float
 int snrse_temb_dense(const float* temb, const float* W, const float* bias, float* out, int B, int R, int D,
                      hipStream_t stream);
 
+/* Fused input conv, bf16 (ncsnpp.py:253-254, 282-285): complex x, y [B][H][W] -> out [B*H*W][128]
+ * bf16 = conv3x3(cat(x.re, x.im, y.re, y.im), wgt) + bias, plus the f32 input pyramid
+ * pyr [B*H*W][4] and out's GroupNorm statistics [B][SLOTS][128][2] (zeroed here unless option
+ * stats_zeroed).  wgt: bf16 [128][64], k = (ky * 3 + kx) * 4 + channel, k >= 36 zero.
+ * Requires W % 64 == 0 and (H * W / 64) % 16 == 0 (else SNRSE_EINVAL: use snrse_input_pack). */
+int snrse_input_conv(const void* x, const void* y, int B, int H, int W, const void* wgt, const float* bias,
+                     void* out, float* pyr, double* stats, hipStream_t stream);
+
 /* Network input (ncsnpp.py:253-254, 282-285): complex x, y [B,F,T] -> im2col [B,F,T,64]
  * (tap-major 3x3 x {x.re, x.im, y.re, y.im}, zero padded) in dtype, and the f32 input
  * pyramid [B,F,T,4]. */

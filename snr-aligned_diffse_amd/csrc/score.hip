@@ -138,6 +138,125 @@ __global__ __launch_bounds__(256) void input_pack_kernel(const float2* x, const 
   *(u32x4*)(col + (size_t)p * 64 + k * VEC) = o;
 }
 
+// ---- fused input conv (bf16): complex (x, y) -> h = conv3x3(4 -> 128) + bias, NHWC bf16 -------
+// (ncsnpp.py:253-254, 282-285).  Replaces input_pack's 64-channel im2col round trip through HBM +
+// a K=64 GEMM: the 36 products per output come from x / y directly (cache-resident neighbours),
+// so the launch is bound by the 256 B/pixel output store.  MFMA 16x16x32 with A = the packed
+// weights [128 co][64 k] (k = tap * 4 + {x.re, x.im, y.re, y.im}, 36..63 zero) and B = the
+// pixels' tap values, so D = [co][px]: each lane holds 4 consecutive channels of one pixel
+// (8-byte bf16 stores, a pixel's 256 B completed by the same wave).  GroupNorm statistics of h:
+// f32 per lane over the workgroup's 16 tiles, DPP row sums, a fixed-order fold of the 4 waves in
+// LDS, one f64 atomic pair per channel per workgroup (slot = blockIdx & 15).  Also writes the f32 input pyramid.
+// Contract: W % 64 == 0, (H * W / 64) % 16 == 0 (a workgroup's 16 tiles lie in one image).
+constexpr int IC_TPW = 4;  // 64-px tiles per wave
+SNRSE_DEV f32x4 mfma_bf16_16x16x32(const u32x4& a, const u32x4& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, a), __builtin_bit_cast(bf16x8_mfma, b),
+                                                 c, 0, 0, 0);
+}
+template <int CTRL>
+SNRSE_DEV float ic_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+SNRSE_DEV float ic_row_sum16(float v) {
+  v += ic_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += ic_dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += ic_dpp<0x141>(v);  // row_half_mirror
+  v += ic_dpp<0x140>(v);  // row_mirror
+  return v;
+}
+
+__global__ __launch_bounds__(256) void input_conv_kernel(const float2* __restrict__ x, const float2* __restrict__ y,
+                                                         int H, int W, const bf16_t* __restrict__ wgt,
+                                                         const float* __restrict__ bias, bf16_t* __restrict__ out,
+                                                         float* __restrict__ pyr, double* __restrict__ stats) {
+  __shared__ float s_st[4][128 * 2];  // per-wave channel sums: fixed-order fold, no LDS atomics
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, lr = lane & 15;
+  u32x4 wf[8][2];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) wf[j][s] = *(const u32x4*)(wgt + (16 * j + lr) * 64 + 32 * s + 8 * g);
+  float bv[8][4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const f32x4 b4 = *(const f32x4*)(bias + 16 * j + 4 * g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bv[j][e] = b4[e];
+  }
+  float s1[8][4], s2[8][4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { s1[j][e] = 0.f; s2[j][e] = 0.f; }
+  const int HW = H * W, tpr = W / 64;
+  const long long tile0 = ((long long)blockIdx.x * 4 + wid) * IC_TPW;
+  const int b = (int)(((long long)blockIdx.x * 16 * 64) / HW);
+  for (int tt = 0; tt < IC_TPW; ++tt) {
+    const long long tile = tile0 + tt;
+    const int rem = (int)(tile - (long long)b * (HW / 64));
+    const int h = rem / tpr, w0 = (rem - h * tpr) * 64;
+    const size_t img = (size_t)b * HW;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int w = w0 + 16 * i + lr;
+      // B fragments: K-step 0 = taps 2g, 2g + 1; K-step 1 = tap 8 (g == 0), zero otherwise
+      u32x4 pf[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int tap = 8 * s + 2 * g + u;
+          float v4[4] = {0.f, 0.f, 0.f, 0.f};
+          if (tap < 9) {
+            const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
+            if (hh >= 0 && hh < H && ww >= 0 && ww < W) {
+              const size_t q = img + (size_t)hh * W + ww;
+              const float2 a = x[q], c = y[q];
+              v4[0] = a.x; v4[1] = a.y; v4[2] = c.x; v4[3] = c.y;
+              if (tap == 4) *(float4*)(pyr + (img + (size_t)h * W + w) * 4) = make_float4(a.x, a.y, c.x, c.y);
+            }
+          }
+          pf[s][2 * u] = pack_bf16x2(v4[0], v4[1]);
+          pf[s][2 * u + 1] = pack_bf16x2(v4[2], v4[3]);
+        }
+      }
+      bf16_t* orow = out + (img + (size_t)h * W + w) * 128 + 4 * g;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc = mfma_bf16_16x16x32(wf[j][0], pf[0], acc);
+        acc = mfma_bf16_16x16x32(wf[j][1], pf[1], acc);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[e] + bv[j][e];
+          s1[j][e] += v[e];
+          s2[j][e] = fmaf(v[e], v[e], s2[j][e]);
+        }
+        uint2 o;
+        o.x = pack_bf16x2(v[0], v[1]);
+        o.y = pack_bf16x2(v[2], v[3]);
+        *(uint2*)(orow + 16 * j) = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a = ic_row_sum16(s1[j][e]), q = ic_row_sum16(s2[j][e]);
+      if (lr == 0) {  // one lane per (wave, channel)
+        s_st[wid][(16 * j + 4 * g + e) * 2] = a;
+        s_st[wid][(16 * j + 4 * g + e) * 2 + 1] = q;
+      }
+    }
+  __syncthreads();
+  const int slot = blockIdx.x & (SNRSE_STAT_SLOTS - 1);
+  const float tot = (s_st[0][tid] + s_st[1][tid]) + (s_st[2][tid] + s_st[3][tid]);
+  unsafeAtomicAdd(&stats[stat_idx(b, slot, tid >> 1, 128) + (tid & 1)], (double)tot);
+}
+
 // ---- Philox4x32-10 -> Box-Muller complex normals -------------------------------------
 SNRSE_DEV uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t& hi) {
   const uint64_t p = (uint64_t)a * b;
@@ -270,6 +389,19 @@ extern "C" int snrse_temb_dense(const float* temb, const float* W, const float* 
   if (D > 512 || D % 4 || B <= 0 || B > 32 || (size_t)B * D * 4 > 64 * 1024) return SNRSE_EINVAL;
   hipLaunchKernelGGL(temb_dense_kernel, dim3((R + 63) / 64), dim3(256), sizeof(float) * B * D, s, temb, W, bias,
                      out, B, R, D);
+  return (int)hipGetLastError();
+}
+
+extern "C" int snrse_input_conv(const void* x, const void* y, int B, int H, int W, const void* wgt, const float* bias,
+                                void* out, float* pyr, double* stats, hipStream_t s) {
+  if (B <= 0 || H <= 0 || W <= 0 || W % 64 || ((long long)H * W / 64) % 16 || !x || !y || !wgt || !bias || !out ||
+      !pyr || !stats)
+    return SNRSE_EINVAL;
+  if (!g_snrse_stats_zeroed)
+    SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * 128, s));
+  const long long blocks = (long long)B * H * W / (64 * 16);
+  hipLaunchKernelGGL(input_conv_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const float2*)x, (const float2*)y,
+                     H, W, (const bf16_t*)wgt, bias, (bf16_t*)out, pyr, stats);
   return (int)hipGetLastError();
 }
 

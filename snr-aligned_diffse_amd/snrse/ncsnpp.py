@@ -23,6 +23,8 @@ import torch
 from . import ops
 
 INV_SQRT2 = 1.0 / math.sqrt(2.0)
+# tests flip this to compare the fused bf16 input conv with the im2col + GEMM path
+_NO_FUSED_INPUT = False
 
 
 @dataclass
@@ -240,8 +242,12 @@ class NCSNppHIP:
     def _pyramid(self, x, y, t):
         W = self.W
         dense = self.temb(t)
-        col, pyr_in = ops.input_pack(x, y, self.dtype)
-        h = self._conv(col, W["in_w"], 1, 128, bias=W["in_b"])
+        if self.dtype == torch.bfloat16 and ops.input_conv_ok(x) and not _NO_FUSED_INPUT:
+            ht, hst, pyr_in = ops.input_conv(x, y, W["in_w"], W["in_b"])
+            h = (ht, hst)
+        else:
+            col, pyr_in = ops.input_pack(x, y, self.dtype)
+            h = self._conv(col, W["in_w"], 1, 128, bias=W["in_b"])
         hs = [h]
         plan = self.plan
         i = 4

@@ -314,6 +314,24 @@ def temb_dense(temb, W, bias):
     return out
 
 
+def input_conv_ok(x):
+    B, F, T = x.shape[0], x.shape[-2], x.shape[-1]
+    return T % 64 == 0 and (F * T // 64) % 16 == 0
+
+
+def input_conv(x, y, wgt, bias):
+    """bf16 fused input conv: x, y complex64 [B,F,T] -> (h [B,F,T,128] bf16, stats, pyramid f32)."""
+    _dev(x, y, wgt, bias)
+    B, F, T = x.shape[0], x.shape[-2], x.shape[-1]
+    h = torch.empty(B, F, T, 128, device=x.device, dtype=torch.bfloat16)
+    pyr = torch.empty(B, F, T, 4, device=x.device, dtype=torch.float32)
+    st = new_stats(B, 128)
+    _stats_zeroed(st)
+    _lib.call("snrse_input_conv", x.data_ptr(), y.data_ptr(), B, F, T, wgt.data_ptr(), bias.data_ptr(),
+              h.data_ptr(), pyr.data_ptr(), st.data_ptr(), _stream())
+    return h, st, pyr
+
+
 def input_pack(x, y, dtype):
     """x, y complex64 [B,F,T] -> (im2col [B,F,T,64] dtype, pyramid [B,F,T,4] f32)."""
     _dev(x, y)

@@ -525,3 +525,34 @@ def test_stats_arena_repeat_evaluations(gpu, sd_ncsnpp, dt):
     s0, _ = ops.gn_stats(nhwc(torch.ones(2, 128, 8, 64, device=gpu, dtype=DT[dt][0])))
     assert ops.get_option("stats_zeroed") == 0
     assert torch.allclose(ops.fold_stats(s0)[..., 0], torch.full((2, 128), 512.0, device=gpu, dtype=torch.float64))
+
+
+def test_input_conv_fused_vs_im2col_gemm(gpu):
+    """snrse_input_conv (fused bf16 input conv, ncsnpp.py:253-254, 282-285) against the
+    input_pack im2col + K=64 GEMM path on the same packed weights: h to bf16 rounding, the
+    GroupNorm statistics to 1e-3 relative, the input pyramid exactly."""
+    from snrse import ops
+    g = torch.Generator().manual_seed(5)
+    B, F, T = 2, 256, 128
+    x = torch.complex(torch.randn(B, F, T, generator=g), torch.randn(B, F, T, generator=g)).to(gpu)
+    y = torch.complex(torch.randn(B, F, T, generator=g), torch.randn(B, F, T, generator=g)).to(gpu)
+    w = torch.randn(128, 36, generator=g) / 6
+    wp = torch.cat([w, torch.zeros(128, 28)], 1).bfloat16().to(gpu).contiguous()
+    bias = (torch.randn(128, generator=g) * 0.1).to(gpu)
+    h, st, pyr = ops.input_conv(x, y, wp, bias)
+    col, pyr0 = ops.input_pack(x, y, torch.bfloat16)
+    st0 = ops.new_stats(B, 128)
+    h0 = ops.conv2d(col, wp, 1, 128, bias=bias, stats=st0)
+    torch.cuda.synchronize()
+    assert torch.equal(pyr, pyr0)
+    d = (h.float() - h0.float()).abs().max().item()
+    assert d <= 2 ** -7 * h0.float().abs().max().item(), d
+    s, s0 = st.sum(1), st0.sum(1)  # fold the slots: [B, 128, 2]
+    assert torch.allclose(s, s0, rtol=1e-3, atol=1e-2 * float(s0.abs().max()) * 1e-3)
+    # reference arithmetic on the host (fp32 conv of the bf16-rounded inputs and weights)
+    xin = torch.stack([x.real, x.imag, y.real, y.imag], 1).cpu().bfloat16().float()
+    wt = wp[:, :36].float().cpu().reshape(128, 3, 3, 4).permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(xin, wt, bias.cpu(), padding=1).permute(0, 2, 3, 1)
+    assert (h.float().cpu() - ref).abs().max().item() <= 2 ** -7 * ref.abs().max().item()
+    ok_shape = torch.zeros(1, 8, 64, dtype=torch.complex64, device=gpu)
+    assert not ops.input_conv_ok(ok_shape)  # 8 x 64 px = 8 tiles: outside the contract
