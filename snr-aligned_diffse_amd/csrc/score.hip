@@ -143,8 +143,8 @@ __global__ __launch_bounds__(256) void input_pack_kernel(const float2* x, const 
 // a K=64 GEMM: the 36 products per output come from x / y directly (cache-resident neighbours),
 // so the launch is bound by the 256 B/pixel output store.  MFMA 16x16x32 with A = the packed
 // weights [128 co][64 k] (k = tap * 4 + {x.re, x.im, y.re, y.im}, 36..63 zero) and B = the
-// pixels' tap values, so D = [co][px]: each lane holds 4 consecutive channels of one pixel
-// (8-byte bf16 stores, a pixel's 256 B completed by the same wave).  GroupNorm statistics of h:
+// pixels' tap values, so D = [co][px]: each lane holds 4 consecutive channels of one pixel; a
+// row swap pairs them into 8 (16-byte stores, a pixel's 256 B completed by the same wave).  GroupNorm statistics of h:
 // f32 per lane over the workgroup's 16 tiles, DPP row sums, a fixed-order fold of the 4 waves in
 // LDS, one f64 atomic pair per channel per workgroup (slot = blockIdx & 15).  Also writes the f32 input pyramid.
 // Contract: W % 64 == 0, (H * W / 64) % 16 == 0 (a workgroup's 16 tiles lie in one image).
@@ -192,38 +192,65 @@ __global__ __launch_bounds__(256) void input_conv_kernel(const float2* __restric
   const int HW = H * W, tpr = W / 64;
   const long long tile0 = ((long long)blockIdx.x * 4 + wid) * IC_TPW;
   const int b = (int)(((long long)blockIdx.x * 16 * 64) / HW);
-  for (int tt = 0; tt < IC_TPW; ++tt) {
-    const long long tile = tile0 + tt;
+  const size_t img = (size_t)b * HW;
+  // this lane's taps: 2g, 2g + 1 (K-step 0) and 8 (K-step 1, g == 0 only)
+  int tdy[3], tdx[3];
+  bool tuse[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int tap = u < 2 ? 2 * g + u : 8;
+    tuse[u] = u < 2 || g == 0;
+    tdy[u] = tap / 3 - 1;
+    tdx[u] = tap % 3 - 1;
+  }
+  // 16 pixel blocks of 16 px per wave, software-pipelined: block q + 1's neighbour loads are
+  // issued before block q's stores, so waiting for them never waits for those stores
+  // (vmcnt counts stores too on gfx950)
+  auto load_blk = [&](int q, float2 (&lx)[3], float2 (&ly)[3], bool (&ok)[3]) {
+    const long long tile = tile0 + (q >> 2);
     const int rem = (int)(tile - (long long)b * (HW / 64));
-    const int h = rem / tpr, w0 = (rem - h * tpr) * 64;
-    const size_t img = (size_t)b * HW;
+    const int h = rem / tpr, w = (rem - h * tpr) * 64 + 16 * (q & 3) + lr;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int w = w0 + 16 * i + lr;
-      // B fragments: K-step 0 = taps 2g, 2g + 1; K-step 1 = tap 8 (g == 0), zero otherwise
-      u32x4 pf[2];
+    for (int u = 0; u < 3; ++u) {
+      const int hh = h + tdy[u], ww = w + tdx[u];
+      ok[u] = tuse[u] && hh >= 0 && hh < H && ww >= 0 && ww < W;
+      const size_t qq = img + (ok[u] ? (size_t)hh * W + ww : (size_t)h * W + w);
+      lx[u] = x[qq];
+      ly[u] = y[qq];
+    }
+  };
+  float2 cx[3], cy[3];
+  bool cok[3];
+  load_blk(0, cx, cy, cok);
+  for (int q = 0; q < 4 * IC_TPW; ++q) {
+    float2 nx[3], ny[3];
+    bool nok[3];
+    if (q + 1 < 4 * IC_TPW) load_blk(q + 1, nx, ny, nok);
+    const long long tile = tile0 + (q >> 2);
+    const int rem = (int)(tile - (long long)b * (HW / 64));
+    const int h = rem / tpr, w = (rem - h * tpr) * 64 + 16 * (q & 3) + lr;
+    u32x4 pf[2];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+    for (int u = 0; u < 3; ++u) {
+      const float2 a = cok[u] ? cx[u] : make_float2(0.f, 0.f);
+      const float2 c = cok[u] ? cy[u] : make_float2(0.f, 0.f);
+      const int sl = u < 2 ? 0 : 1, hw_ = u < 2 ? 2 * u : 0;
+      pf[sl][hw_] = pack_bf16x2(a.x, a.y);
+      pf[sl][hw_ + 1] = pack_bf16x2(c.x, c.y);
+    }
+    pf[1][2] = 0u;
+    pf[1][3] = 0u;
+    if (g == 2)  // tap 4 = the pixel itself: the input pyramid
+      *(float4*)(pyr + (img + (size_t)h * W + w) * 4) = make_float4(cx[0].x, cx[0].y, cy[0].x, cy[0].y);
+    // channel blocks (2jp, 2jp + 1) are exchanged between DPP rows (v_permlane16_swap) so each lane
+    // stores 8 consecutive channels: 16-B stores, 64 contiguous bytes of a pixel per instruction
+    bf16_t* orow = out + (img + (size_t)h * W + w) * 128 + 8 * (g >> 1);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int tap = 8 * s + 2 * g + u;
-          float v4[4] = {0.f, 0.f, 0.f, 0.f};
-          if (tap < 9) {
-            const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
-            if (hh >= 0 && hh < H && ww >= 0 && ww < W) {
-              const size_t q = img + (size_t)hh * W + ww;
-              const float2 a = x[q], c = y[q];
-              v4[0] = a.x; v4[1] = a.y; v4[2] = c.x; v4[3] = c.y;
-              if (tap == 4) *(float4*)(pyr + (img + (size_t)h * W + w) * 4) = make_float4(a.x, a.y, c.x, c.y);
-            }
-          }
-          pf[s][2 * u] = pack_bf16x2(v4[0], v4[1]);
-          pf[s][2 * u + 1] = pack_bf16x2(v4[2], v4[3]);
-        }
-      }
-      bf16_t* orow = out + (img + (size_t)h * W + w) * 128 + 4 * g;
+    for (int jp = 0; jp < 4; ++jp) {
+      uint32_t pk[2][2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int hh = 0; hh < 2; ++hh) {
+        const int j = 2 * jp + hh;
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
         acc = mfma_bf16_16x16x32(wf[j][0], pf[0], acc);
         acc = mfma_bf16_16x16x32(wf[j][1], pf[1], acc);
@@ -234,11 +261,19 @@ __global__ __launch_bounds__(256) void input_conv_kernel(const float2* __restric
           s1[j][e] += v[e];
           s2[j][e] = fmaf(v[e], v[e], s2[j][e]);
         }
-        uint2 o;
-        o.x = pack_bf16x2(v[0], v[1]);
-        o.y = pack_bf16x2(v[2], v[3]);
-        *(uint2*)(orow + 16 * j) = o;
+        pk[hh][0] = pack_bf16x2(v[0], v[1]);
+        pk[hh][1] = pack_bf16x2(v[2], v[3]);
       }
+      const auto r0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+      const auto r1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+      const u32x4 o = {r0[0], r1[0], r0[1], r1[1]};
+      *(u32x4*)(orow + 16 * (2 * jp + (g & 1))) = o;
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      cx[u] = nx[u];
+      cy[u] = ny[u];
+      cok[u] = nok[u];
     }
   }
 #pragma unroll
