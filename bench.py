@@ -57,6 +57,18 @@ def formula_weights():
     return {k: torch.from_numpy(v) for k, v in formula.formula_state_dict(shapes).items()}
 
 
+def snrnet_formula(dev):
+    """SNRNet (sgmse/backbones/snrnet.py) with formula weights of the reference architecture."""
+    from snrse import formula
+    from sgmse.backbones import SNRNet
+    with open(os.path.join(ROOT, "tests", "golden", "state_dict_keys.json")) as f:
+        shapes = {"snrnet." + k: tuple(s) for k, s in json.load(f)["snrnet"]}
+    sd = {k[len("snrnet."):]: torch.from_numpy(v) for k, v in formula.formula_state_dict(shapes).items()}
+    net = SNRNet()
+    net.load_state_dict(sd)
+    return net
+
+
 def cpu_baseline(seconds=4.0, nfe=2, threads=None):
     """Oracle (CPU restatement) on a bounded sample: 1 clip, `nfe` NCSN++ evaluations + the
     STFT/iSTFT and SDE updates, extrapolated to 60 NFE per utterance."""
@@ -164,6 +176,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--conv-variant", type=int, default=0, help="snrse conv_variant option (0 = auto)")
+    ap.add_argument("--config", choices=["c2", "c4"], default="c2",
+                    help="c2: PC sampler (default, the headline line); c4: one-step SNR-aligned path "
+                         "(SNRNet estimate + 1 preconditioned NFE, sebridge_v3)")
     args = ap.parse_args()
 
     from snrse import dist as sdist
@@ -182,6 +197,12 @@ def main():
     B = args.batch
     y = torch.from_numpy(synth_clips(B, args.seconds, 1000 * rank)).to(dev)
     noise = lambda it: sampler.NoiseSource(seed=7919 * (rank + 1) + it)  # noqa: E731
+    if args.config == "c4":
+        from snrse.enhance import SNRAlignedEnhancer
+        snr_net = snrnet_formula(dev)
+        one = SNRAlignedEnhancer(net, snr_fn=lambda spec: (lambda g: g / (1 - g))(snr_net.forward_complex(spec)[:, 0]),
+                                 fixed_snr=0.17783, sigma_max=0.5)
+        enh = lambda yy, nz: (one(yy, seed=nz.seed)[0], 1)  # noqa: E731
 
     for w in range(args.warmup):
         enh(y, noise(w))
@@ -228,12 +249,12 @@ def main():
                                        for k, v in by.items() if k != kname}}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         cpu = cpu_baseline()
 
     n_frames = 1 + int(args.seconds * SR) // 128
     T_frames = (n_frames + 63) // 64 * 64
-    cfg = "C2" if (args.seconds == 4.0 and args.dtype == "bf16") else (
+    cfg = "C4" if args.config == "c4" else "C2" if (args.seconds == 4.0 and args.dtype == "bf16") else (
         "C5" if args.seconds >= 30 and args.dtype == "fp32" else "custom")
     if rank == 0:
         line = {
@@ -241,8 +262,11 @@ def main():
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (SURVEY §8d harmonic+noise clips; formula weights of the NCSN++ architecture)",
-            "config": {"workload": f"{cfg}: B={B} {args.seconds:g} s/16 kHz clips per GPU, N={args.N} PC steps "
-                                   f"(reverse_diffusion + ald, {nfe} NFE/utt), OUVE SDE, NCSN++ nf=128",
+            "config": {"workload": (f"{cfg}: B={B} {args.seconds:g} s/16 kHz clips per GPU, one-step SNR-aligned "
+                                    f"enhancement (SNRNet estimate + 1 sebridge_v3 NFE at t_hat), NCSN++ nf=128")
+                       if args.config == "c4" else
+                       (f"{cfg}: B={B} {args.seconds:g} s/16 kHz clips per GPU, N={args.N} PC steps "
+                        f"(reverse_diffusion + ald, {nfe} NFE/utt), OUVE SDE, NCSN++ nf=128"),
                        "global_batch": B * world, "per_gpu_batch": B, "seq_len": T_frames,
                        "parallelism": f"dp{world} (utterance sharding)"},
             "roofline": roof, "cpu_baseline": cpu,

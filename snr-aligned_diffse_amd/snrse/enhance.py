@@ -71,3 +71,36 @@ class PCEnhancer:
         Y = ops.stft(y, 1.0, tpad=pad_frames(T), mode=1, in_div=nf)
         x, nfe = self.sample(Y, noise)
         return ops.istft(x, L, mode=1, out_scale=nf), nfe
+
+
+class SNRAlignedEnhancer:
+    """One-step SNR-aligned enhancement of a batch (C4: model_type 'sebridge_v3',
+    snr_conditioned 'true'; model.py:713-740, 810-833), the reference's per-utterance loop as one
+    batched pass: y / max|y| -> raw STFT padded to 16 frames -> SNR estimate (`snr_fn`, e.g.
+    SNRNet's forward_complex -> g / (1 - g), or oracle noise/clean rms) -> t_hat snapped to t_30
+    -> Y = spec_fwd(STFT(y / (max|y| normfac))) -> X_T = Y + sigma_max t_hat Z -> one
+    preconditioned NCSN++ evaluation at t_hat (c_skip x + c_out dnn, score mode 1) -> iSTFT x
+    max|y| normfac.  The per-utterance scalars (t_hat, normfac) are host float64 as in the
+    reference (one B-element copy).  Returns (x_hat [B, L], t_hat numpy [B])."""
+
+    def __init__(self, net, snr_fn=None, fixed_snr=0.17783, sigma_max=0.5):
+        self.net, self.snr_fn = net, snr_fn
+        self.fixed_snr, self.sigma_max = float(fixed_snr), float(sigma_max)
+
+    def __call__(self, y, est_snr=None, noise=None, seed=0):
+        B, L = y.shape
+        nf = ops.absmax(y)
+        if est_snr is None:
+            T16 = pad_frames(1 + L // 128, 16)
+            raw = ops.stft(y, 1.0, tpad=T16, mode=0, in_div=nf)  # no spec transform (model.py:715-719)
+            est_snr = self.snr_fn(raw).reshape(B).double().cpu().numpy()
+        t_hat = snap_t(est_snr, self.fixed_snr)
+        div = nf * torch.from_numpy(normfac(t_hat, self.fixed_snr)).to(nf.device, torch.float32)
+        Y = ops.stft(y, 1.0, tpad=pad_frames(1 + L // 128), mode=1, in_div=div)
+        coef = torch.zeros(B, 4, dtype=torch.float32)
+        coef[:, 1] = 1.0
+        coef[:, 3] = torch.from_numpy(self.sigma_max * t_hat).float()
+        X_T = ops.axpby_noise(coef.to(Y.device), y=Y, noise=noise, seed=seed)
+        tv = torch.from_numpy(t_hat).to(Y.device, torch.float32)
+        sample = self.net.score(X_T, Y, tv, 1)
+        return ops.istft(sample.contiguous(), L, mode=1, out_scale=div.contiguous()), t_hat
