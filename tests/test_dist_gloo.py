@@ -54,3 +54,63 @@ def test_gloo_world2_gather():
     assert (a0, b0, a1, b1) == (0, 4, 4, 7)
     assert t0 == t1 == 2.0
     assert m0 == m1 == [[float(i), float(i) * 0.5] for i in range(n_total)]
+
+
+def _eval_worker(rank, world, port, root, out, q):
+    """evaluate() on gloo with a stand-in model and metric (the HIP parts are GPU-tested in
+    test_metrics.py): each rank enhances its shard, the rows meet in one all_gather, rank 0 writes."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import numpy as np
+
+    from snrse import dist as sd
+    from snrse import evaluate as ev
+    r, w, _ = sd.init_from_env("gloo")
+
+    class _SDE:
+        _T = 1.0
+
+    class _Model:
+        sde = _SDE()
+        seen = []
+
+        def enhance(self, x, y, **kw):
+            self.seen.append(kw["N"])
+            return (0.5 * y[0]).numpy()
+
+    ev.score_files = lambda xh, x, y, sr=16000, pesq_fn=None: [float("nan"), float(len(x)), float(r), float(xh[0])]
+    m = _Model()
+    data = ev.evaluate(m, root, out, N=30, rank=r, world=w)
+    q.put((r, len(m.seen), data["si_sdr"], data["si_sir"]))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_gloo_world2_evaluate_sharded(tmp_path):
+    import numpy as np
+
+    from snrse import audio
+    root = tmp_path / "t"
+    for d in ("clean", "noisy"):
+        os.makedirs(root / d)
+    for k in range(5):
+        sig = np.full(1000 + 10 * k, 0.25, np.float32)
+        audio.write_wav(str(root / "clean" / f"u{k}.wav"), sig, bits=32)
+        audio.write_wav(str(root / "noisy" / f"u{k}.wav"), sig, bits=32)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    out = str(tmp_path / "out")
+    procs = [ctx.Process(target=_eval_worker, args=(r, 2, port, str(root), out, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, n0, sdr0, sir0), (r1, n1, sdr1, sir1) = res
+    assert (n0, n1) == (3, 2)                       # contiguous shards of the 5 files
+    assert sdr0 == sdr1 == [1000.0 + 10 * k for k in range(5)]  # every row, in file order
+    assert sir0 == [0.0, 0.0, 0.0, 1.0, 1.0]        # which rank scored each file
+    lines = open(os.path.join(out, "_results.csv")).read().splitlines()
+    assert len(lines) == 6 and lines[1].startswith("u0.wav,nan,1000.0,0.0,")
