@@ -1029,6 +1029,10 @@ int launch_halo(ConvParams p, hipStream_t s) {
 // prologue / epilogue runs under the other's MFMAs (v4 is 1 workgroup/CU, 152 KB).
 SNRSE_DEV int swz64(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >> 1) & 3)) << 4); }
 
+#ifndef SNRSE_H5_PRIO
+#define SNRSE_H5_PRIO 0  // measured 1-2 % slower with the priority bump (tools/conv_bench.py A/B): off
+#endif
+constexpr bool g_h5_prio_dev = SNRSE_H5_PRIO;  // s_setprio around the MFMA block of each tap
 SNRSE_DEV int h5_opaque(int v) {
   int r;
   asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
@@ -1248,12 +1252,15 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
       for (int i = 0; i < 4; ++i) af[i] = *(const u32x4*)(halo + swz64(hbase + i * 16, lg));
 #pragma unroll
       for (int j = 0; j < 8; ++j) bfr[j] = *(const u32x4*)(sb + swz64(j * 16 + lrow, lg));
+      if (g_h5_prio_dev) __builtin_amdgcn_s_setprio(1);  // favour the MFMA stream over the co-resident
+                                                        // workgroup's transform / epilogue waves
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[h][i][j] = mfma_chunk<bf16_t>(af[i], bfr[h * 4 + j], acc[h][i][j]);
+      if (g_h5_prio_dev) __builtin_amdgcn_s_setprio(0);
     }
     SNRSE_STAMP(3 + 2 * (q & 15));
     if (last && c + 1 < ncb) {
