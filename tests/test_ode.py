@@ -132,3 +132,18 @@ def test_ode_sampler_hip_vs_scipy_loop():
     torch.manual_seed(7)
     x_dn, _ = sampling.get_ode_sampler(sde, m, Y, rtol=rtol, atol=atol, eps=0.03)()
     assert x_dn.shape == Y.shape and torch.isfinite(torch.view_as_real(x_dn)).all()
+
+
+@pytest.mark.gpu
+def test_enhance_ode_branch():
+    """ScoreModel.enhance(sampler_type='ode') (model.py:762-763): the eval.py kwargs (atol, rtol,
+    timestep_type, correct_stepsize) flow through to the device RK45; output is a finite waveform
+    of the input length."""
+    from test_gpu_dropin import score_model
+
+    m = score_model("bbed", dtype="fp32")
+    L = 9000
+    y = (0.1 * torch.sin(torch.arange(L) * 0.05) + 0.01 * torch.randn(L, generator=torch.Generator().manual_seed(1)))
+    x_hat = m.enhance(y[None], y[None], sampler_type="ode", N=30, atol=1e-3, rtol=1e-3, timestep_type="linear",
+                      correct_stepsize=False)
+    assert x_hat.shape == (L,) and np.isfinite(x_hat).all()
