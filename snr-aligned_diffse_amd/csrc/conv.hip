@@ -239,10 +239,30 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
   float s1[EPC], s2[EPC];
 #pragma unroll
   for (int k = 0; k < EPC; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+  // bf16: every pass's residual / Combine input is loaded up front, so the passes do not wait on
+  // one HBM round trip each (a wait that, vmcnt being in order, also drained the earlier stores)
+  constexpr int NPASS = 64 / RPP;
+#ifndef SNRSE_EPI_PREFETCH
+#define SNRSE_EPI_PREFETCH 1
+#endif
+  constexpr bool PRE = SNRSE_EPI_PREFETCH && sizeof(TO) == 2;
+  u32x4 rpre[PRE ? NPASS : 1];
+  f32x4 qpre[PRE ? NPASS : 1];
+  if constexpr (PRE) {
+    if (p.res) {
+#pragma unroll
+      for (int pass = 0; pass < NPASS; ++pass)
+        rpre[pass] = *(const u32x4*)((const TO*)p.res + ((size_t)mb + r0 + pass * RPP) * p.res_ld + n);
+    }
+    if (p.comb_src) {
+#pragma unroll
+      for (int pass = 0; pass < NPASS; ++pass) qpre[pass] = *(const f32x4*)(p.comb_src + ((size_t)mb + r0 + pass * RPP) * 4);
+    }
+  }
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
-  for (int pass = 0; pass < 64 / RPP; ++pass) {
+  for (int pass = 0; pass < NPASS; ++pass) {
     const int row = r0 + pass * RPP;
     const size_t m = (size_t)mb + row;
     float v[EPC];
@@ -250,7 +270,9 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
 #pragma unroll
     for (int k = 0; k < EPC; ++k) v[k] = sr[k] + add[k];
     if (p.res) {
-      const u32x4 rv = *(const u32x4*)((const TO*)p.res + m * p.res_ld + n);
+      u32x4 rv;
+      if constexpr (PRE) rv = rpre[pass];
+      else rv = *(const u32x4*)((const TO*)p.res + m * p.res_ld + n);
       if constexpr (sizeof(TO) == 2) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -265,7 +287,9 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
 #pragma unroll
     for (int k = 0; k < EPC; ++k) v[k] *= p.out_scale;
     if (p.comb_src) {
-      const f32x4 q = *(const f32x4*)(p.comb_src + m * 4);
+      f32x4 q;
+      if constexpr (PRE) q = qpre[pass];
+      else q = *(const f32x4*)(p.comb_src + m * 4);
 #pragma unroll
       for (int k = 0; k < EPC; ++k) v[k] += q[0] * cw[k][0] + q[1] * cw[k][1] + q[2] * cw[k][2] + q[3] * cw[k][3] + cb[k];
     }
