@@ -1067,6 +1067,116 @@ SNRSE_DEV int h5_opaque(int v) {
 // workgroups per CU per launch keep each count's parity = arrival order
 __device__ unsigned g_h5_cu_arrivals[8 * 256];
 
+#ifndef SNRSE_H5_SWAP
+#define SNRSE_H5_SWAP 0  // swapped operands + register epilogue: correct but 3 % slower (scattered 16-B stores; A/B ABA 12.05/12.03 vs 12.41 utt/s): off
+#endif
+template <int CTRL>
+SNRSE_DEV float h5_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// sum over the 16 lanes of a DPP row (every lane of the row receives it)
+SNRSE_DEV float h5_row_sum16(float v) {
+  v += h5_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += h5_dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += h5_dpp<0x141>(v);  // row_half_mirror
+  v += h5_dpp<0x140>(v);  // row_mirror
+  return v;
+}
+
+// v5 epilogue with swapped MFMA operands (D = [co][px], lane (g = lane >> 4, lr = lane & 15) of
+// block (h, i, j) holds channels n0 + 64h + 16j + 4g + e of pixel 16i + lr): the accumulators of
+// channel blocks (2jp, 2jp + 1) are exchanged between DPP rows (v_permlane16_swap), so every lane
+// owns 8 consecutive channels of one pixel -- bias / temb / residual / Combine and the 16-byte
+// store straight from registers, no LDS staging.  GroupNorm statistics: per-lane sums over the 4
+// pixel blocks, DPP row sums over the 16 pixels, one LDS row per wave for block_stats_flush.
+template <typename TO>
+SNRSE_DEV void epilogue_swapped(const ConvParams& p, const f32x4 (&acc)[2][4][4], int mrow, int n0, int lane,
+                                float* red, int wid, int b) {
+  const int g = lane >> 4, lr = lane & 15;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      const int nl = 64 * h + 16 * (2 * jp + (g & 1)) + 8 * (g >> 1);  // channel offset within the tile
+      const int n = n0 + nl;
+      float add[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) add[k] = 0.f;
+      if (p.bias) {
+        const f32x4 b0 = *(const f32x4*)(p.bias + n), b1 = *(const f32x4*)(p.bias + n + 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { add[k] += b0[k]; add[k + 4] += b1[k]; }
+      }
+      if (p.temb) {
+        const float* tb = p.temb + (size_t)b * p.temb_stride + n;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) add[k] += tb[k];
+      }
+      u32x4 rv[4];
+      f32x4 qv[4];
+      if (p.res) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rv[i] = *(const u32x4*)((const TO*)p.res + ((size_t)mrow + 16 * i + lr) * p.res_ld + n);
+      }
+      if (p.comb_src) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) qv[i] = *(const f32x4*)(p.comb_src + ((size_t)mrow + 16 * i + lr) * 4);
+      }
+      float s1[8], s2[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        f32x4 a = acc[h][i][2 * jp], bq = acc[h][i][2 * jp + 1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[e]), __float_as_uint(bq[e]), false, false);
+          a[e] = __uint_as_float(r[0]);
+          bq[e] = __uint_as_float(r[1]);
+        }
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { v[e] = a[e] + add[e]; v[e + 4] = bq[e] + add[e + 4]; }
+        if (p.res) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[2 * k] += __uint_as_float(rv[i][k] << 16);
+            v[2 * k + 1] += __uint_as_float(rv[i][k] & 0xffff0000u);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] *= p.out_scale;
+        if (p.comb_src) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const f32x4 w = *(const f32x4*)(p.comb_w + (size_t)(n + k) * 4);
+            v[k] += qv[i][0] * w[0] + qv[i][1] * w[1] + qv[i][2] * w[2] + qv[i][3] * w[3] + p.comb_b[n + k];
+          }
+        }
+        const u32x4 o = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                         pack_bf16x2(v[6], v[7])};
+        TO* dst = (TO*)p.out + ((size_t)mrow + 16 * i + lr) * p.out_ld + n;
+        if (p.epi_nt) __builtin_nontemporal_store(o, (u32x4*)dst);
+        else *(u32x4*)dst = o;
+        if (p.stats) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { s1[k] += v[k]; s2[k] = fmaf(v[k], v[k], s2[k]); }
+        }
+      }
+      if (p.stats) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float a1 = h5_row_sum16(s1[k]), a2 = h5_row_sum16(s2[k]);
+          if (lr == 0) {
+            red[(wid * 128 + nl + k) * 2] = a1;
+            red[(wid * 128 + nl + k) * 2 + 1] = a2;
+          }
+        }
+      }
+    }
+  }
+}
+
 // GroupNorm prologue of the v5 halo kernel on one packed bf16 pair: GNM 1 = affine, 2 = affine + SiLU
 template <int GNM>
 SNRSE_DEV uint32_t gn_xform2(uint32_t v, float s0, float h0, float s1, float h1) {
@@ -1082,6 +1192,7 @@ SNRSE_DEV uint32_t gn_xform2(uint32_t v, float s0, float h0, float s1, float h1)
 
 template <typename TO, int GNM>
 __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
+  constexpr bool H5SW = SNRSE_H5_SWAP && sizeof(TO) == 2;  // swapped operands + register epilogue
   constexpr int TH = 4, TW = 64, HC = TW + 2;
   constexpr int HROWS = (TH + 2) * HC;  // 396
   constexpr int HJ = 7;                 // halo rows per thread: (tid >> 2) + 64 j
@@ -1283,7 +1394,9 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[h][i][j] = mfma_chunk<bf16_t>(af[i], bfr[h * 4 + j], acc[h][i][j]);
+          for (int j = 0; j < 4; ++j)
+            acc[h][i][j] = H5SW ? mfma_chunk<bf16_t>(bfr[h * 4 + j], af[i], acc[h][i][j])   // D[co][px]
+                                : mfma_chunk<bf16_t>(af[i], bfr[h * 4 + j], acc[h][i][j]);  // D[px][co]
       if (g_h5_prio_dev) __builtin_amdgcn_s_setprio(0);
     }
     SNRSE_STAMP(3 + 2 * (q & 15));
@@ -1299,11 +1412,15 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   float* const stage = (float*)(smem + wid * (64 * 68 * 4));
   float* const red = (float*)(smem + 4 * (64 * 68 * 4));
   const int mrow = (bb * p.H + h0 + wid) * p.W + w0;
-  epilogue_img<TO, 4, 128, true>(p, acc[0], mrow, n0, lane, stage, red, wid, bb, n0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  SNRSE_STAMP(26);
-  epilogue_img<TO, 4, 128, true>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0);
+  if constexpr (H5SW) {
+    epilogue_swapped<TO>(p, acc, mrow, n0, lane, red, wid, bb);
+  } else {
+    epilogue_img<TO, 4, 128, true>(p, acc[0], mrow, n0, lane, stage, red, wid, bb, n0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    SNRSE_STAMP(26);
+    epilogue_img<TO, 4, 128, true>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0);
+  }
   SNRSE_STAMP(27);
   if (p.stats) block_stats_flush<4, 128>(p, red, bb, n0);
   }  // tile loop
