@@ -1503,14 +1503,16 @@ int launch_conv(ConvParams p, int npad, hipStream_t s) {
 float* g_ws = nullptr;   // split-K workspace (snrse_set_workspace)
 size_t g_ws_bytes = 0;
 int g_splitk = 1;        // option "splitk": 0 disables K splitting
+int g_splitk_target = 256;  // option "splitk_target": workgroups a split-K launch aims for (swept
+                            // 128/192/256/512/1024 on C2: 256 best, split-K off is 9 % slower)
 int g_last_ksplit = 1;   // option read-back "last_ksplit": splits of the latest v2 launch
 
 // K splits for a v2 launch of `tiles` output tiles over nk K-tiles: about one workgroup per CU when
 // the tile grid alone underfills the chip (the small NCSN++ levels), >= 4 K-tiles per split, and
 // the partial sums within the registered workspace
 int choose_ksplit(const ConvParams& p, int tiles, int nk) {
-  if (!g_splitk || !g_ws || tiles >= 192) return 1;
-  int s = (256 + tiles - 1) / tiles;
+  if (!g_splitk || !g_ws || tiles >= g_splitk_target * 3 / 4) return 1;
+  int s = (g_splitk_target + tiles - 1) / tiles;
   if (s > nk / 4) s = nk / 4;
   const size_t plane = (size_t)p.M * p.Cout * sizeof(float);
   if ((size_t)s * plane > g_ws_bytes) s = (int)(g_ws_bytes / plane);
@@ -1685,6 +1687,7 @@ extern "C" int snrse_set_option(const char* name, int value) {
   if (!name) return SNRSE_EINVAL;
   if (name_is(name, "conv_variant")) { g_conv_variant = value; return 0; }
   if (name_is(name, "splitk")) { g_splitk = value; return 0; }
+  if (name_is(name, "splitk_target")) { g_splitk_target = value > 0 ? value : 256; return 0; }
   if (name_is(name, "h5_persist")) { g_h5_persist = value; return 0; }
   if (name_is(name, "epi_nt")) { g_epi_nt = value; return 0; }
   if (name_is(name, "h5_stagger")) { g_h5_stagger_per_phase = value; return 0; }
