@@ -4,15 +4,22 @@
 One "step" = ScoreModel.enhance() on one batch of B synthetic 4 s / 16 kHz noisy clips:
 device STFT + exponent transform -> prior -> N=30 PC steps (reverse_diffusion predictor +
 ALD corrector = 60 NCSN++ NFEs, each fused with its SDE update) -> iSTFT.  Inputs are
-resident in HBM before the timed region.  Multi-GPU: one process per GPU (torchrun), each
-rank enhances its own batch (weak scaling, utterance sharding, no collective in the data
-path); RCCL is used for the max-over-ranks time and the final metric gather only.
+resident in HBM before the timed region.
 
-Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement for the roofline definition.
+Multi-GPU (`--gpus N`): one process per GPU.  Launched by torchrun (RANK / WORLD_SIZE in the
+environment) the ranks are torchrun's; otherwise bench.py starts the N ranks itself
+(snrse.dist.spawn_ranks, before anything touches the GPU).  Each rank enhances its own batch
+(weak scaling, utterance sharding, no collective in the data path); RCCL is used for the
+max-over-ranks time and the final metric gather only.
+
+Configs (BASELINE.json): c2 (default, the headline line), c4 (SNR-aligned one-step path),
+c5 (30 s clips, N=200, fp32), and `--gpus 0` = c1 (the reference's CPU plumbing case, run by the
+CPU oracle: no GPU).  Prints ONE JSON line (rank 0).  See DESIGN.md §4 for the roofline definition.
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import math
 import os
@@ -50,55 +57,205 @@ def synth_clips(n, seconds, seed0):
     return out
 
 
+def _shapes(kind):
+    with open(os.path.join(ROOT, "tests", "golden", "state_dict_keys.json")) as f:
+        return json.load(f)[kind]
+
+
 def formula_weights():
     from snrse import formula
-    with open(os.path.join(ROOT, "tests", "golden", "state_dict_keys.json")) as f:
-        shapes = {k: tuple(s) for k, s in json.load(f)["ncsnpp"]}
+    shapes = {k: tuple(s) for k, s in _shapes("ncsnpp")}
     return {k: torch.from_numpy(v) for k, v in formula.formula_state_dict(shapes).items()}
+
+
+def snrnet_formula_sd():
+    from snrse import formula
+    shapes = {"snrnet." + k: tuple(s) for k, s in _shapes("snrnet")}
+    return {k[len("snrnet."):]: torch.from_numpy(v) for k, v in formula.formula_state_dict(shapes).items()}
 
 
 def snrnet_formula(dev):
     """SNRNet (sgmse/backbones/snrnet.py) with formula weights of the reference architecture."""
-    from snrse import formula
     from sgmse.backbones import SNRNet
-    with open(os.path.join(ROOT, "tests", "golden", "state_dict_keys.json")) as f:
-        shapes = {"snrnet." + k: tuple(s) for k, s in json.load(f)["snrnet"]}
-    sd = {k[len("snrnet."):]: torch.from_numpy(v) for k, v in formula.formula_state_dict(shapes).items()}
     net = SNRNet()
-    net.load_state_dict(sd)
+    net.load_state_dict(snrnet_formula_sd())
     return net
 
 
-def cpu_baseline(seconds=4.0, nfe=2, threads=None):
-    """Oracle (CPU restatement) on a bounded sample: 1 clip, `nfe` NCSN++ evaluations + the
-    STFT/iSTFT and SDE updates, extrapolated to 60 NFE per utterance."""
-    from oracle import ncsnpp_ref, spec_ref
-    threads = threads or min(16, os.cpu_count() or 1)
+# ----------------------------------------------------------------------------- CPU baseline
+def cpu_threads():
+    """Host threads this process may actually run on: the affinity mask, capped by a cgroup-v2 CPU
+    quota (a GPU box shares its host; os.cpu_count() reports the whole machine there, and torch
+    threads beyond the quota only time-slice)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_env():
+    threads = cpu_threads()
     torch.set_num_threads(threads)
+    return {"cores": threads, "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count()}
+
+
+def _complex_noise(gen):
+    def noise(shape):  # torch.randn_like on complex64: each part N(0, 1/2)
+        return torch.complex(torch.randn(shape, generator=gen), torch.randn(shape, generator=gen)) * math.sqrt(0.5)
+    return noise
+
+
+def cpu_baseline(seconds=4.0, n_steps=2, full=False):
+    """The oracle (CPU restatement of the reference path, pinned to the reference goldens) on the
+    host: one synthetic 4 s clip, STFT + exponent transform -> prior -> `n_steps` PC steps with the
+    reference's reverse_diffusion + ALD algebra (sde_ref.pc_sample: 2 fp32 NCSN++ NFEs per step) ->
+    spec_back + iSTFT.  The per-NFE time (step algebra included) is extrapolated to N=30 (60 NFE).
+    full=True also runs the whole N=30 utterance once and reports it beside the extrapolation."""
+    from oracle import ncsnpp_ref, sde_ref, spec_ref
+    env = _cpu_env()
     sd = ncsnpp_ref.state_dict_to_torch({k: v.numpy() for k, v in formula_weights().items()})
     y = synth_clips(1, seconds, 10_000)
-    t0 = time.perf_counter()
-    Y = spec_ref.spec_fwd(spec_ref.stft(y / np.abs(y).max()))
-    Y = torch.from_numpy(spec_ref.pad_spec(Y).astype(np.complex64))[:, None]
-    t_front = time.perf_counter() - t0
-    x = Y.clone()
-    tt = torch.tensor([0.5])
+    gen = torch.Generator().manual_seed(0)
+    noise = _complex_noise(gen)
+    sde = sde_ref.OUVE(theta=1.5, sigma_min=0.05, sigma_max=0.5, N=30)
+
+    def score_fn(x, t, Y):  # ScoreModel.forward, model_type 'bbed' (model.py:488-489)
+        return -ncsnpp_ref.ncsnpp_forward(torch.cat([x, Y], 1), torch.full((x.shape[0],), float(t)), sd)
+
+    def front():
+        nf = np.abs(y).max()
+        Y = spec_ref.spec_fwd(spec_ref.stft(y / nf))
+        return torch.from_numpy(spec_ref.pad_spec(Y).astype(np.complex64))[:, None], nf
+
+    def back(x, nf):
+        return spec_ref.istft(spec_ref.spec_back(x[0, 0].numpy()), y.shape[1]) * nf
+
     with torch.no_grad():
-        ncsnpp_ref.ncsnpp_forward(torch.cat([x, Y], 1), tt, sd)  # warm-up
         t0 = time.perf_counter()
-        for _ in range(nfe):
-            s = -ncsnpp_ref.ncsnpp_forward(torch.cat([x, Y], 1), tt, sd)
-            x = x + 0.01 * s + 0.01 * torch.randn_like(x)
-        t_nfe = (time.perf_counter() - t0) / nfe
-    t0 = time.perf_counter()
-    spec_ref.istft(spec_ref.spec_back(x[0, 0].numpy()), y.shape[1])
-    t_back = time.perf_counter() - t0
-    t_utt = 60 * t_nfe + t_front + t_back
-    return {"value": 1.0 / t_utt, "unit": "utt/s", "cores": threads, "kind": "port",
-            "sample": f"1 synthetic 4 s clip: {nfe} timed NCSN++ fp32 NFEs (+1 warm-up) at [1,2,256,512] "
-                      f"+ STFT/iSTFT, extrapolated to 60 NFE/utt ({t_nfe:.2f} s/NFE)"}
+        Y, nf = front()
+        t_front = time.perf_counter() - t0
+        score_fn(Y, 0.5, Y)  # warm-up NFE (allocator, oneDNN primitive cache)
+        t0 = time.perf_counter()
+        x, nfe = sde_ref.pc_sample(sde, score_fn, Y, noise, N=n_steps, eps=0.03, snr=0.5)
+        t_loop = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        back(x, nf)
+        t_back = time.perf_counter() - t0
+        t_nfe = t_loop / nfe
+        t_utt = t_front + 60 * t_nfe + t_back
+        res = {"value": 1.0 / t_utt, "unit": "utt/s", "cores": env["cores"], "kind": "port",
+               "sample": (f"1 synthetic {seconds:g} s clip through the oracle (CPU restatement, fp32): STFT + "
+                          f"transform, {n_steps} reverse_diffusion+ALD PC steps ({nfe} NCSN++ NFEs at "
+                          f"[1,2,256,512] with the reference step algebra) + iSTFT; {t_nfe:.2f} s/NFE "
+                          f"extrapolated to N=30 (60 NFE/utt)"),
+               "s_per_nfe": t_nfe, "cpu_model": env["cpu_model"], "os_cpu_count": env["os_cpu_count"]}
+        if full:
+            t0 = time.perf_counter()
+            Y, nf = front()
+            x, nfe_full = sde_ref.pc_sample(sde, score_fn, Y, noise, N=30, eps=0.03, snr=0.5)
+            back(x, nf)
+            t_full = time.perf_counter() - t0
+            res["full_utterance"] = {"N": 30, "nfe": nfe_full, "seconds": t_full, "utt_per_s": 1.0 / t_full,
+                                     "extrapolated_seconds": t_utt, "measured_over_extrapolated": t_full / t_utt}
+    return res
 
 
+def cpu_validation():
+    """Latest committed full-utterance CPU run (bench.py --cpu-full writes profiles/*_cpu_full_n30.json)."""
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_cpu_full_n30.json")))
+    if not paths:
+        return None
+    with open(paths[-1]) as f:
+        d = json.load(f)
+    d["source"] = os.path.relpath(paths[-1], ROOT)
+    return d
+
+
+def c1_clip():
+    """C1's '4 s VBD utterance': the three dataset utterances held in tests/golden/enhance_snrnet_c4.npz
+    (reference dataset/VBD*, 16 kHz int16) concatenated and cut at 4 s."""
+    g = np.load(os.path.join(ROOT, "tests", "golden", "enhance_snrnet_c4.npz"), allow_pickle=False)
+    return (np.concatenate(list(g["noisy_i16"]))[: 4 * SR].astype(np.float32) / 32768.0)[None]
+
+
+def run_c1(args):
+    """configs[0]: the reference's CPU-runnable case, --gpus 0.  One 4 s VBD utterance, sebridge_v3,
+    exponent transform, SNR from SNRNet, on PyTorch CPU via the oracle: the one-step enhance
+    (model.py:713-833; N is ignored on this branch) timed `--steps` times, plus one N=5 PC run
+    (10 NFE, model.py:756-768 arithmetic) as the plumbing check of the sampler path."""
+    from oracle import ncsnpp_ref, sde_ref, snrnet_ref, spec_ref
+    env = _cpu_env()
+    sd = ncsnpp_ref.state_dict_to_torch({k: v.numpy() for k, v in formula_weights().items()})
+    ssd = {k: v.float() for k, v in snrnet_formula_sd().items()}
+    y = c1_clip()
+    fixed_snr, sigma_max = 0.17783, 0.5
+    noise = _complex_noise(torch.Generator().manual_seed(1))
+
+    def one_step():
+        nf0 = float(np.abs(y).max())
+        raw = spec_ref.stft(y / nf0)
+        T16 = raw.shape[-1] + (16 - raw.shape[-1] % 16) % 16
+        R = np.zeros((1, 256, T16), np.complex64)
+        R[..., : raw.shape[-1]] = raw
+        Rt = torch.from_numpy(R)
+        g = snrnet_ref.snrnet_forward(torch.stack([Rt.real, Rt.imag], 1), ssd)
+        est = float(g[0, 0] / (1 - g[0, 0]))
+        t_hat = snrnet_ref.snap_t(est, fixed_snr)
+        norm = nf0 * snrnet_ref.normfac(t_hat, fixed_snr)
+        Y = torch.from_numpy(spec_ref.pad_spec(spec_ref.spec_fwd(spec_ref.stft(y / norm))).astype(np.complex64))[:, None]
+        X = Y + noise(Y.shape) * sigma_max * t_hat
+        tt = torch.tensor([t_hat], dtype=torch.float32)
+        c_skip = 0.25 / ((t_hat - 0.001) ** 2 + 0.25)
+        c_out = 0.5 * (t_hat - 0.001) / math.sqrt(0.25 + t_hat ** 2)
+        s = c_skip * X + c_out * ncsnpp_ref.ncsnpp_forward(torch.cat([X, Y], 1), tt, sd)
+        return spec_ref.istft(spec_ref.spec_back(s[0, 0].numpy()), y.shape[1]) * norm, t_hat
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            one_step()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            xh, t_hat = one_step()
+        el = time.perf_counter() - t0
+        Y = torch.from_numpy(spec_ref.pad_spec(spec_ref.spec_fwd(spec_ref.stft(y / np.abs(y).max())))
+                             .astype(np.complex64))[:, None]
+        t1 = time.perf_counter()
+        xp, ns = sde_ref.pc_sample(sde_ref.OUVE(1.5, 0.05, 0.5, N=5), lambda x, t, Yc: -ncsnpp_ref.ncsnpp_forward(
+            torch.cat([x, Yc], 1), torch.full((1,), float(t)), sd), Y, noise, N=5)
+        t_pc = time.perf_counter() - t1
+    value = args.steps / el
+    cpu = {"value": value, "unit": "utt/s", "cores": env["cores"], "kind": "port",
+           "sample": f"C1 itself: {args.steps} one-step enhancements of the 4 s VBD clip",
+           "cpu_model": env["cpu_model"], "os_cpu_count": env["os_cpu_count"]}
+    line = {"metric": METRIC, "value": value, "unit": "utt/s", "n_gpus": 0, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "VBD dataset utterances (reference dataset/, via tests/golden) cut to 4 s; formula weights",
+            "config": {"workload": ("C1: one 4 s VBD utterance, sebridge_v3 + snr_conditioned (SNRNet estimate), "
+                                    "exponent transform, one-step enhance on PyTorch CPU (oracle restatement; "
+                                    "--gpus 0 plumbing, no GPU)"),
+                       "global_batch": 1, "per_gpu_batch": 1, "seq_len": 512, "parallelism": "none (CPU)"},
+            "roofline": None, "cpu_baseline": cpu, "t_hat": float(t_hat),
+            "output_rms": float(np.sqrt(np.mean(np.asarray(xh, np.float64) ** 2))),
+            "pc_n5_plumbing": {"nfe": ns, "seconds": t_pc, "finite": bool(torch.isfinite(torch.view_as_real(xp)).all())}}
+    print(json.dumps(line), flush=True)
+
+
+# ----------------------------------------------------------------------------- roofline probe
 def conv_flops(src0, src1, ksize, cout, sc, sc1):
     B, H, W, C0 = src0.shape
     cin = C0 + (0 if src1 is None else src1.shape[3])
@@ -107,11 +264,11 @@ def conv_flops(src0, src1, ksize, cout, sc, sc1):
 
 
 class ConvProbe:
-    """HIP events on the launch stream around every halo-path conv launch (bf16 3x3, Cout % 128 == 0,
-    H % 4 == 0, W % 64 == 0; ops.halo_ok) during one extra enhance() pass after the timed region,
-    grouped by the kernel that ran (snrse_get_option "last_kernel").  achieved = algorithmic FLOPs of
-    the dominant kernel's launches / their summed event time, i.e. mean FLOPs per launch / mean
-    launch duration (the quantity rocprofv3 --stats reports as AverageNs for that kernel)."""
+    """HIP events on the launch stream around every big conv launch during one extra enhance() pass
+    after the timed region (bf16: the halo-path 3x3 convs, ops.halo_ok; fp32 parity mode: every 3x3
+    conv with Cout >= 64), grouped by the kernel that ran (snrse_get_option "last_kernel").
+    achieved = algorithmic FLOPs of the dominant kernel's launches / their summed event time, i.e. mean
+    FLOPs per launch / mean launch duration (the quantity rocprofv3 --stats reports as AverageNs)."""
 
     def __init__(self):
         self.rec = []
@@ -121,7 +278,6 @@ class ConvProbe:
         probe = self
 
         def wrapped(src0, wgt, ksize, cout, *a, **kw):
-            # bf16: the halo-path convs; fp32 parity mode (C5): every 3x3 conv with Cout >= 64
             big = ops.halo_ok(src0, ksize, cout) or (src0.dtype == torch.float32 and ksize == 3 and cout >= 64)
             if not big:
                 return orig(src0, wgt, ksize, cout, *a, **kw)
@@ -151,38 +307,29 @@ class ConvProbe:
         return by
 
 
-def pmc_traffic(kernel_prefix):
+def pmc_traffic(kernel_prefix, tag):
     """HBM bytes per launch of the dominant kernel from the committed PMC profile
-    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950
-    correction + WRITE_SIZE); None when absent."""
-    import glob
+    (profiles/*_pmc_traffic.json, tools/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950 correction +
+    WRITE_SIZE) for this config tag; None when absent."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
         with open(path) as f:
             d = json.load(f)
-        if d.get("kernel", "").startswith(kernel_prefix):
+        if d.get("kernel", "").startswith(kernel_prefix) and d.get("config", "c2") == tag:
             return d.get("bytes_per_launch"), os.path.relpath(path, ROOT)
     return None, None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=32, help="utterances per GPU")
-    ap.add_argument("--N", type=int, default=30, help="PC steps")
-    ap.add_argument("--seconds", type=float, default=4.0)
-    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-probe", action="store_true")
-    ap.add_argument("--conv-variant", type=int, default=0, help="snrse conv_variant option (0 = auto)")
-    ap.add_argument("--config", choices=["c2", "c4"], default="c2",
-                    help="c2: PC sampler (default, the headline line); c4: one-step SNR-aligned path "
-                         "(SNRNet estimate + 1 preconditioned NFE, sebridge_v3)")
-    args = ap.parse_args()
+# ----------------------------------------------------------------------------- GPU bench
+CONFIG_DEFAULTS = {"c2": dict(batch=32, N=30, seconds=4.0, dtype="bf16"),
+                   "c4": dict(batch=32, N=30, seconds=4.0, dtype="bf16"),
+                   "c5": dict(batch=1, N=200, seconds=30.0, dtype="fp32")}
 
+
+def run(args):
     from snrse import dist as sdist
     rank, world, dev = sdist.init_from_env()
+    if world != max(args.gpus, 1):
+        raise SystemExit(f"bench: --gpus {args.gpus} but the process group has {world} ranks")
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -193,7 +340,9 @@ def main():
     ops.set_option("conv_variant", args.conv_variant)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     net = ncsnpp.NCSNppHIP(formula_weights(), dtype=dtype, device=dev)
-    enh = PCEnhancer(net, sampler.SDESpec("ouve", theta=1.5, sigma_min=0.05, sigma_max=0.5), N=args.N)
+    sde = sampler.SDESpec("ouve", theta=1.5, sigma_min=0.05, sigma_max=0.5)
+    enh = PCEnhancer(net, sde, N=args.N)
+    probe_enh = PCEnhancer(net, sde, N=min(args.N, 2))  # kernel durations do not depend on N
     B = args.batch
     y = torch.from_numpy(synth_clips(B, args.seconds, 1000 * rank)).to(dev)
     noise = lambda it: sampler.NoiseSource(seed=7919 * (rank + 1) + it)  # noqa: E731
@@ -202,7 +351,7 @@ def main():
         snr_net = snrnet_formula(dev)
         one = SNRAlignedEnhancer(net, snr_fn=lambda spec: (lambda g: g / (1 - g))(snr_net.forward_complex(spec)[:, 0]),
                                  fixed_snr=0.17783, sigma_max=0.5)
-        enh = lambda yy, nz: (one(yy, seed=nz.seed)[0], 1)  # noqa: E731
+        enh = probe_enh = lambda yy, nz: (one(yy, seed=nz.seed)[0], 1)  # noqa: E731
 
     for w in range(args.warmup):
         enh(y, noise(w))
@@ -232,42 +381,47 @@ def main():
         probe = ConvProbe()
         probe.install(ops)
         try:
-            enh(y, noise(999))
+            probe_enh(y, noise(999))
         finally:
             probe.uninstall()
         by = probe.summary()
-        kname = max(by, key=lambda k: by[k][1])  # the halo kernel with the most time in the step
+        kname = max(by, key=lambda k: by[k][1])  # the conv kernel with the most time in the pass
         fl, ms, n = by[kname]
         ach = fl / (ms * 1e-3) if ms > 0 else 0.0
         peak = PEAK[args.dtype]
-        traffic, tsrc = pmc_traffic(kname)
+        traffic, tsrc = pmc_traffic(kname, args.config)
         roof = {"bound": "mfma", "achieved": ach / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
-                "frac": ach / peak, "traffic": traffic, "kernel": kname, "launches_per_step": n,
+                "frac": ach / peak, "traffic": traffic, "kernel": kname, "launches_per_pass": n,
                 "avg_launch_us": ms * 1e3 / max(n, 1), "flop_per_launch": fl / max(n, 1),
-                "kernel_ms_per_step": ms, "traffic_source": tsrc,
-                "other_halo_kernels": {k: {"launches": v[2], "ms": v[1], "tflops": v[0] / max(v[1], 1e-9) / 1e9}
+                "kernel_ms_per_pass": ms, "traffic_source": tsrc,
+                "other_conv_kernels": {k: {"launches": v[2], "ms": v[1], "tflops": v[0] / max(v[1], 1e-9) / 1e9}
                                        for k, v in by.items() if k != kname}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         cpu = cpu_baseline()
+        val = cpu_validation()
+        if val is not None:
+            cpu["validation"] = val
 
     n_frames = 1 + int(args.seconds * SR) // 128
     T_frames = (n_frames + 63) // 64 * 64
-    cfg = "C4" if args.config == "c4" else "C2" if (args.seconds == 4.0 and args.dtype == "bf16") else (
-        "C5" if args.seconds >= 30 and args.dtype == "fp32" else "custom")
+    tag = args.config.upper()
+    if args.config == "c2" and (args.seconds != 4.0 or args.dtype != "bf16" or args.N != 30):
+        tag = "custom"
     if rank == 0:
+        if args.config == "c4":
+            wl = (f"C4: B={B} {args.seconds:g} s/16 kHz clips per GPU, one-step SNR-aligned enhancement "
+                  f"(SNRNet estimate + 1 sebridge_v3 NFE at t_hat), NCSN++ nf=128")
+        else:
+            wl = (f"{tag}: B={B} {args.seconds:g} s/16 kHz clips per GPU, N={args.N} PC steps "
+                  f"(reverse_diffusion + ald, {nfe} NFE/utt), OUVE SDE, NCSN++ nf=128, {args.dtype}")
         line = {
             "metric": METRIC, "value": value, "unit": "utt/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (SURVEY §8d harmonic+noise clips; formula weights of the NCSN++ architecture)",
-            "config": {"workload": (f"{cfg}: B={B} {args.seconds:g} s/16 kHz clips per GPU, one-step SNR-aligned "
-                                    f"enhancement (SNRNet estimate + 1 sebridge_v3 NFE at t_hat), NCSN++ nf=128")
-                       if args.config == "c4" else
-                       (f"{cfg}: B={B} {args.seconds:g} s/16 kHz clips per GPU, N={args.N} PC steps "
-                        f"(reverse_diffusion + ald, {nfe} NFE/utt), OUVE SDE, NCSN++ nf=128"),
-                       "global_batch": B * world, "per_gpu_batch": B, "seq_len": T_frames,
+            "config": {"workload": wl, "global_batch": B * world, "per_gpu_batch": B, "seq_len": T_frames,
                        "parallelism": f"dp{world} (utterance sharding)"},
             "roofline": roof, "cpu_baseline": cpu,
             "output_rms_mean": float(allm.mean()),
@@ -278,5 +432,43 @@ def main():
         dist.destroy_process_group()
 
 
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1, help="GPUs (ranks); 0 = C1, the CPU plumbing case")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", choices=["c2", "c4", "c5"], default="c2",
+                    help="c2: PC sampler, B=32 4 s bf16 (default, the headline line); c4: one-step SNR-aligned "
+                         "path (SNRNet estimate + 1 preconditioned NFE, sebridge_v3); c5: 30 s clips, N=200, fp32")
+    ap.add_argument("--batch", type=int, default=None, help="utterances per GPU")
+    ap.add_argument("--N", type=int, default=None, help="PC steps")
+    ap.add_argument("--seconds", type=float, default=None)
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--conv-variant", type=int, default=0, help="snrse conv_variant option (0 = auto)")
+    ap.add_argument("--cpu-full", default=None, metavar="PATH",
+                    help="only run the CPU baseline with one full N=30 utterance and write it to PATH")
+    args = ap.parse_args()
+    for k, v in CONFIG_DEFAULTS[args.config].items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+    if args.cpu_full:
+        res = cpu_baseline(full=True)
+        with open(args.cpu_full, "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res), flush=True)
+        return 0
+    if args.gpus == 0:
+        run_c1(args)
+        return 0
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # start the N ranks here (no torchrun); nothing in this process has touched the GPU
+        from snrse import dist as sdist
+        return sdist.spawn_ranks(args.gpus, run, (args,))
+    run(args)
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

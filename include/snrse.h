@@ -26,7 +26,7 @@ extern "C" {
 
 typedef struct ihipStream_t* hipStream_t;
 
-enum { SNRSE_F32 = 0, SNRSE_BF16 = 1 };
+enum { SNRSE_F32 = 0, SNRSE_BF16 = 1, SNRSE_F16 = 2, SNRSE_F64 = 3 };
 
 int snrse_abi_version(void);
 const char* snrse_error_string(int code);
@@ -37,7 +37,9 @@ int snrse_device_name(char* buf, int len);
  * pad_y0, pad_y1) (op/upfirdn2d.cpp:12-23, op/upfirdn2d_kernel.cu:209-369, semantics of
  * upfirdn2d_native op/upfirdn2d.py:159-200).  `kernel` is [kh, kw] f32 on the device;
  * `out` is caller-allocated [major, out_h, out_w, minor] with
- * out_h = (in_h*up_y + pad_y0 + pad_y1 - kh)/down_y + 1 (out_w likewise). */
+ * out_h = (in_h*up_y + pad_y0 + pad_y1 - kh)/down_y + 1 (out_w likewise).
+ * dtype: SNRSE_F32 / SNRSE_F16 / SNRSE_F64, the reference's float / half / double dispatch
+ * (upfirdn2d_kernel.cu:311), plus SNRSE_BF16; f64 accumulates in f64, the others in f32. */
 int snrse_upfirdn2d(const void* in, void* out, const float* kernel, int major, int in_h, int in_w,
                     int minor, int kh, int kw, int up_x, int up_y, int down_x, int down_y,
                     int pad_x0, int pad_x1, int pad_y0, int pad_y1, int dtype, hipStream_t stream);

@@ -66,7 +66,7 @@ SNRSE_DEV double wave_sum_d(double v) {
 }
 
 // dtype codes shared with the C-ABI (include/snrse.h)
-enum { SNRSE_F32 = 0, SNRSE_BF16 = 1 };
+enum { SNRSE_F32 = 0, SNRSE_BF16 = 1, SNRSE_F16 = 2, SNRSE_F64 = 3 };  // F16 / F64: snrse_upfirdn2d only
 
 // GroupNorm statistics buffers are [B][SNRSE_STAT_SLOTS][C][2] doubles: producers spread
 // their atomics over the slots (a few hundred workgroups per image would otherwise queue on

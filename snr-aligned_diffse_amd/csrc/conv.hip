@@ -21,6 +21,7 @@
 // kernel needs because its fragments start at arbitrary (tap-shifted) rows.
 #include "conv_common.h"
 
+#include <algorithm>
 #include <type_traits>
 
 using namespace snrse_conv;
@@ -800,251 +801,6 @@ __global__ __launch_bounds__(256) void conv_splitk_finalize(ConvParams p, int pp
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// v4 (bf16, 3x3, H % 4 == 0, W % 64 == 0): halo tiles with fused GroupNorm-apply + SiLU.
-// Output tile = 4 frequency rows x 64 frames (256 pixels) x 128 output channels, 8 waves of
-// 64x64.  Per 64-channel block (cb) the (4+2) x (64+2) input halo is loaded ONCE through
-// registers (prefetched one phase ahead), normalised + SiLU'd there when the conv consumes
-// SiLU(GN(x)) (ResBlock Conv_0 / Conv_1, layerspp.py:245, 266), and written to a single
-// LDS halo image that all 9 taps read at shifted rows (row&7 swizzle: conflict-free for any
-// 16-row window).  Weight tiles stream by LDS-DMA into a 2-slot ring, three taps per slot,
-// so each barrier is followed by 96 MFMAs per wave.  1x1 shortcut K-blocks (Conv_2 of the
-// same ResBlock) run as one-tap phases over the raw shortcut input.
-// LDS: 56 KiB halo + 2 x 48 KiB weights = 152 KiB (one 512-thread block per CU).
-template <typename TO, bool LDS_EPI>
-__global__ __launch_bounds__(512) void conv_halo_kernel(ConvParams p) {
-  constexpr int TH = 4, TW = 64, HC = TW + 2;
-  constexpr int HROWS = (TH + 2) * HC;       // 396
-  constexpr int HJ = 7;                      // 16-B halo chunks per thread (448 rows x 8 / 512)
-  constexpr int HALO_BYTES = 448 * 128;      // 57344
-  constexpr int TAPB = 128 * 128;            // one tap's 128 x 64 bf16 weight tile
-  constexpr int SLOT = 3 * TAPB;
-  constexpr int FM = 4, FN = 4, KT = 64;
-  static_assert(8 * HJ * 8 >= HROWS, "halo rows");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const halo = smem;
-  char* const ring = smem + HALO_BYTES;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
-#ifdef SNRSE_STAMPS
-  unsigned long long* const lst = (unsigned long long*)(ring + 2 * SLOT) + wid * 32;
-#endif
-  SNRSE_STAMP(0);
-  const int nb = gridDim.x, bid = blockIdx.x;
-  const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7, pos = bid >> 3;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
-  const int n0 = (wg % p.ntn) * 128;
-  int tile = wg / p.ntn;
-  const int ntw = p.W / TW, nth = p.H / TH;
-  const int w0 = (tile % ntw) * TW;
-  tile /= ntw;
-  const int h0 = (tile % nth) * TH;
-  const int bb = tile / nth;
-
-  const int Cin = p.C0 + p.C1;
-  const int cbm = Cin / KT;
-  const int Csc_all = p.Csc + p.Csc1;
-  const int cbs = p.sc_src ? Csc_all / KT : 0;
-  const int ncb = cbm + cbs;
-  const int nq = 3 * cbm + cbs;
-  const int K1 = 9 * Cin;
-  const int slot = lane & 7;
-  const int csel = slot ^ (lane >> 3);  // source chunk of this lane (row & 7 == lane >> 3)
-  const bool gn = p.gn_scale != nullptr;
-
-  int hpix[HJ];
-  bool hok[HJ];
-#pragma unroll
-  for (int j = 0; j < HJ; ++j) {
-    const int hr = (wid * HJ + j) * 8 + (lane >> 3);
-    const int hy = hr / HC, hx = hr - (hr / HC) * HC;
-    const int ih = h0 + hy - 1, iw = w0 + hx - 1;
-    hok[j] = hr < HROWS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
-    hpix[j] = (bb * p.H + ih) * p.W + iw;
-  }
-
-  u32x4 hv[HJ];
-  float gsc[8], gsh[8];
-
-  // ---- halo(c) -> registers (+ this lane's 8 GN scale/shift values)
-#define SNRSE_HALO_LOADS(BASE_, BYTES_, CS_, CC_)                                                      \
-  do {                                                                                              \
-    const __amdgpu_buffer_rsrc_t r_ = make_rsrc((BASE_), (BYTES_));                                 \
-    const int cs_ = (CS_), cc_ = (CC_) + csel * 8;                                                  \
-    _Pragma("unroll") for (int j = 0; j < HJ; ++j) {                                                \
-      const int voff_ = hok[j] ? (hpix[j] * cs_ + cc_) * 2 : (int)0x80000000;                       \
-      hv[j] = __builtin_amdgcn_raw_buffer_load_b128(r_, voff_, 0, 0);                               \
-    }                                                                                               \
-  } while (0)
-  auto halo_load = [&](int c) {
-    if (c < cbm) {
-      const int ch = c * KT;
-      if (ch < p.C0) SNRSE_HALO_LOADS(p.src0, p.bytes0, p.C0, ch);
-      else SNRSE_HALO_LOADS(p.src1, p.bytes1, p.C1, ch - p.C0);
-      if (gn) {
-        const float* sp = p.gn_scale + (size_t)bb * Cin + ch + csel * 8;
-        const float* hp = p.gn_shift + (size_t)bb * Cin + ch + csel * 8;
-        const f32x4 s0 = *(const f32x4*)sp, s1 = *(const f32x4*)(sp + 4);
-        const f32x4 t0 = *(const f32x4*)hp, t1 = *(const f32x4*)(hp + 4);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { gsc[i] = s0[i]; gsc[4 + i] = s1[i]; gsh[i] = t0[i]; gsh[4 + i] = t1[i]; }
-      }
-    } else {
-      const int ch = (c - cbm) * KT;
-      if (ch < p.Csc) SNRSE_HALO_LOADS(p.sc_src, p.sc_bytes0, p.Csc, ch);
-      else SNRSE_HALO_LOADS(p.sc_src1, p.sc_bytes1, p.Csc1, ch - p.Csc);
-    }
-  };
-#undef SNRSE_HALO_LOADS
-  // ---- registers -> (GN + SiLU) -> LDS halo image
-  auto halo_store = [&](int c) {
-    const bool tr = gn && c < cbm;
-#pragma unroll
-    for (int j = 0; j < HJ; ++j) {
-      u32x4 v = hv[j];
-      if (tr) {
-        if (hok[j]) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float lo = __uint_as_float(v[i] << 16), hi = __uint_as_float(v[i] & 0xffff0000u);
-            lo = fmaf(lo, gsc[2 * i], gsh[2 * i]);
-            hi = fmaf(hi, gsc[2 * i + 1], gsh[2 * i + 1]);
-            if (p.gn_act) { lo = silu(lo); hi = silu(hi); }
-            v[i] = pack_bf16x2(lo, hi);
-          }
-        } else {
-          v = u32x4{0u, 0u, 0u, 0u};
-        }
-      }
-      *(u32x4*)(halo + ((wid * HJ + j) * 8 + (lane >> 3)) * 128 + slot * 16) = v;
-    }
-  };
-  // ---- weights of phase q -> ring slot q & 1 (LDS-DMA)
-  auto wload = [&](int q) {
-    int c, t0, nt;
-    if (q < 3 * cbm) { c = q / 3; t0 = (q - c * 3) * 3; nt = 3; }
-    else { c = cbm + (q - 3 * cbm); t0 = 4; nt = 1; }
-    const bool mainw = c < cbm;
-    const int wld = mainw ? K1 : Csc_all;
-    const int kb = mainw ? c * KT : (c - cbm) * KT;
-    const __amdgpu_buffer_rsrc_t r = mainw ? make_rsrc(p.wgt, p.wbytes) : make_rsrc(p.sc_wgt, p.sc_wbytes);
-    char* dst = ring + (q & 1) * SLOT;
-    for (int jt = 0; jt < nt; ++jt) {
-      const int koff = c < cbm ? (t0 + jt) * Cin + kb : kb;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int row = (wid * 2 + i) * 8 + (lane >> 3);
-        const unsigned voff = (unsigned)(((n0 + row) * wld + koff + (slot ^ (row & 7)) * 8) * 2);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            r, (__attribute__((address_space(3))) void*)(dst + jt * TAPB + (wid * 2 + i) * 1024), 16, voff, 0, 0, 0);
-      }
-    }
-  };
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  halo_load(0);
-  wload(0);
-  halo_store(0);
-  SNRSE_STAMP(1);
-  const int lrow = lane & 15, lg = lane >> 4;
-  for (int q = 0; q < nq; ++q) {
-    int c, t0, nt;
-    if (q < 3 * cbm) { c = q / 3; t0 = (q - c * 3) * 3; nt = 3; }
-    else { c = cbm + (q - 3 * cbm); t0 = 4; nt = 1; }
-    const bool first = c < cbm ? t0 == 0 : true;
-    const bool last = c < cbm ? t0 == 6 : true;
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    SNRSE_STAMP(2 + 2 * (q & 15));
-    if (q + 1 < nq) wload(q + 1);
-    if (first && c + 1 < ncb) halo_load(c + 1);
-    const char* sl = ring + (q & 1) * SLOT;
-    for (int jt = 0; jt < nt; ++jt) {
-      const int tp = t0 + jt;
-      const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
-      const int hbase = (wm + dy + 1) * HC + dx + 1 + lrow;
-      const char* sb = sl + jt * TAPB;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        u32x4 af[FM], bfr[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) af[i] = *(const u32x4*)(halo + swz(hbase + i * 16, 4 * k + lg));
-#pragma unroll
-        for (int j = 0; j < FN; ++j) bfr[j] = *(const u32x4*)(sb + swz(wn * 64 + j * 16 + lrow, 4 * k + lg));
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<bf16_t>(af[i], bfr[j], acc[i][j]);
-      }
-    }
-    SNRSE_STAMP(3 + 2 * (q & 15));
-    if (last && c + 1 < ncb) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // every wave is done reading halo(c)
-      halo_store(c + 1);
-    }
-  }
-#ifdef SNRSE_STAMPS
-  SNRSE_STAMP(28);
-  unsigned long long st_[29];
-  if (lane == 0)
-    for (int i = 0; i < 29; ++i) st_[i] = lst[i];
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-#endif
-  if constexpr (LDS_EPI) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // LDS is reused as the epilogue staging area
-    epilogue_img<TO, 4, 128, false>(p, acc, (bb * p.H + h0 + wm) * p.W + w0, n0 + wn * 64, lane,
-                                    (float*)(smem + wid * (64 * 68 * 4)), (float*)(smem + 8 * (64 * 68 * 4)), wm,
-                                    bb, n0);
-  } else {
-    epilogue<TO, FM, FN>(p, acc, (bb * p.H + h0 + wm) * p.W + w0, n0 + wn * 64, lane);
-  }
-#ifdef SNRSE_STAMPS
-  {
-    unsigned long long t_end;
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_end)::"memory");
-    unsigned hw, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    if (lane == 0 && p.stamps) {
-      unsigned long long* g = p.stamps + ((size_t)blockIdx.x * 8 + wid) * 32;
-      for (int i = 0; i < 29; ++i) g[i] = st_[i];
-      g[29] = t_end;
-      g[30] = hw;
-      g[31] = xcc;
-    }
-  }
-#endif
-}
-
-template <typename TO, bool LDS_EPI>
-int launch_halo(ConvParams p, hipStream_t s) {
-#ifdef SNRSE_STAMPS
-  constexpr size_t lds = 448 * 128 + 2 * 3 * 128 * 128 + 8 * 32 * 8;
-#else
-  constexpr size_t lds = 448 * 128 + 2 * 3 * 128 * 128;
-#endif
-  static bool attr = false;
-  if (!attr) {
-    SNRSE_RET(hipFuncSetAttribute((const void*)conv_halo_kernel<TO, LDS_EPI>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
-  }
-  p.ntn = p.Cout / 128;
-  const int tiles = p.B * (p.H / 4) * (p.W / 64);
-  hipLaunchKernelGGL((conv_halo_kernel<TO, LDS_EPI>), dim3(tiles * p.ntn), dim3(512), lds, s, p);
-  return (int)hipGetLastError();
-}
-
 // ---------------------------------------------------------------------------------------------
 // v5 halo GEMM, two workgroups per CU.  4 waves; tile = 4 image rows x 64 px x 128 couts; wave w
 // computes output row h0+w (64 px) x all 128 couts (acc 128 VGPRs).  K runs in 32-channel chunks:
@@ -1448,6 +1204,8 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 int g_epi_nt = 2;                     // option "epi_nt": non-temporal epilogue stores of the v5 halo GEMM:
                                       // 0 off, 1 on, 2 when the output exceeds the 256 MB Infinity
                                       // Cache (+1 % on the full-resolution convs, tools/h5_sweep.py)
+int g_last_epi_nt = 0;                // option read-back "last_epi_nt": store flavour of the latest v5 launch
+int g_last_chunks = 1;                // option read-back "last_chunks": launches of the latest snrse_conv2d
 int g_h5_persist = 0;                 // option "h5_persist": persistent staggered v5 launches (measured
                                       // 5-10 % slower than one tile per workgroup: off)
 int g_h5_slots = 512;                 // two workgroups per CU (256 CUs)
@@ -1468,6 +1226,7 @@ int launch_halo5_gn(ConvParams p, hipStream_t s) {
   }
   p.ntn = p.Cout / 128;
   p.epi_nt = g_epi_nt == 2 ? ((long long)p.M * p.out_ld * (long long)sizeof(TO) > (256ll << 20)) : g_epi_nt;
+  g_last_epi_nt = p.epi_nt;
   const int tiles = p.B * (p.H / 4) * (p.W / 64) * p.ntn;
   int grid = tiles;
   p.h5_tiles = 0;
@@ -1544,15 +1303,14 @@ int launch_glds(ConvParams p, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 4 halo w/ scalar epilogue, 5 halo v5,
-// 6 persistent halo v6, 8 ping-pong halo v8 (v6 / v8 fall back to v4 / v5 outside their contract)
+// 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 5 halo v5 (the experimental v3/v4/v6/v8
+// generations live in git history and tools/experimental/, outside the product library)
 int g_conv_variant = 0;
 constexpr int kHaloAuto = 5;  // halo kernel generation taken by variant 0 (fastest measured: profiles/)
 int g_last_kernel = 0;        // option read-back "last_kernel": generation of the latest launch (9 = head)
 
 template <typename T, typename TO>
 int dispatch_conv(const ConvParams& p, hipStream_t s) {
-  const int hk = g_conv_variant == 0 ? kHaloAuto : g_conv_variant;
   if (p.Cout >= 64) {
     if (p.Cout % 128 != 0) return SNRSE_EINVAL;
     if constexpr (sizeof(T) == 2) {
@@ -1560,22 +1318,8 @@ int dispatch_conv(const ConvParams& p, hipStream_t s) {
                         p.sc_bytes1 < 0x7ff00000ll;
       if (g_conv_variant != 1 && fits) {
         if (g_conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0) {
-          if constexpr (sizeof(TO) == 2) {
-            if (hk == 8 && halo8_ok(p)) {
-              g_last_kernel = 8;
-              return launch_halo8(p, s);
-            }
-            if (hk == 6 && halo6_ok(p)) {
-              g_last_kernel = 6;
-              return launch_halo6(p, s);
-            }
-          }
-          if (hk == 5 || hk == 8) {
-            g_last_kernel = 5;
-            return launch_halo5<TO>(p, s);
-          }
-          g_last_kernel = 4;
-          return g_conv_variant == 4 ? launch_halo<TO, false>(p, s) : launch_halo<TO, true>(p, s);
+          g_last_kernel = 5;
+          return launch_halo5<TO>(p, s);
         }
         if (p.gn_scale) return SNRSE_EINVAL;  // fused GroupNorm exists only on the halo paths
         g_last_kernel = 2;
@@ -1645,11 +1389,51 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
   p.sc_wbytes = (long long)npad * (p.Csc + p.Csc1) * esz;
   p.ntn = 1;
   if (stats && !g_snrse_stats_zeroed) SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * Cout, stream));
-  if (dtype == SNRSE_BF16) {
-    return out_f32 ? dispatch_conv<bf16_t, float>(p, stream) : dispatch_conv<bf16_t, bf16_t>(p, stream);
+  if (dtype != SNRSE_BF16 && dtype != SNRSE_F32) return SNRSE_EINVAL;
+  auto run = [&](const ConvParams& q) {
+    if (dtype == SNRSE_BF16)
+      return out_f32 ? dispatch_conv<bf16_t, float>(q, stream) : dispatch_conv<bf16_t, bf16_t>(q, stream);
+    return dispatch_conv<float, float>(q, stream);
+  };
+  // The buffer-resource kernels address each source with a 32-bit byte extent and offset.  Images are
+  // independent (NHWC, batch outermost), so a batch whose sources exceed 2 GiB (e.g. B >= 64 at the
+  // 256 x 512 x 128 level) runs as consecutive launches over image ranges that fit -- the same kernels,
+  // never a silent fallback to the register-staged GEMM.
+  const long long per_img = (long long)H * W * std::max(std::max(C0, C1), std::max(p.Csc, p.Csc1)) * esz;
+  constexpr long long kLim = 0x7ff00000ll;
+  g_last_chunks = 1;
+  if (per_img * B < kLim || per_img >= kLim) return run(p);
+  const int chunk = (int)((kLim - 1) / per_img);
+  g_last_chunks = (B + chunk - 1) / chunk;
+  const long long HWl = (long long)H * W;
+  for (int b0 = 0; b0 < B; b0 += chunk) {
+    const int nb = std::min(chunk, B - b0);
+    ConvParams q = p;
+    const long long px0 = (long long)b0 * HWl;
+    auto off = [&](const void* ptr, long long elems, long long bytes_per) -> const void* {
+      return ptr ? (const void*)((const char*)ptr + elems * bytes_per) : nullptr;
+    };
+    const long long osz = (dtype == SNRSE_BF16 && !out_f32) ? 2 : 4;
+    q.src0 = off(p.src0, px0 * C0, esz);
+    q.src1 = off(p.src1, px0 * C1, esz);
+    q.sc_src = off(p.sc_src, px0 * p.Csc, esz);
+    q.sc_src1 = off(p.sc_src1, px0 * p.Csc1, esz);
+    q.res = off(p.res, px0 * res_ld, osz);
+    q.comb_src = (const float*)off(p.comb_src, px0 * 4, 4);
+    q.out = (void*)off(p.out, px0 * out_ld, osz);
+    q.temb = (const float*)off(p.temb, (long long)b0 * temb_stride, 4);
+    q.stats = p.stats ? p.stats + (size_t)b0 * SNRSE_STAT_SLOTS * Cout * 2 : nullptr;
+    q.gn_scale = (const float*)off(p.gn_scale, (long long)b0 * (C0 + C1), 4);
+    q.gn_shift = (const float*)off(p.gn_shift, (long long)b0 * (C0 + C1), 4);
+    q.B = nb;
+    q.M = nb * H * W;
+    const long long qpix = (long long)nb * HWl;
+    q.bytes0 = qpix * C0 * esz; q.bytes1 = qpix * C1 * esz;
+    q.sc_bytes0 = qpix * p.Csc * esz; q.sc_bytes1 = qpix * p.Csc1 * esz;
+    const int rc = run(q);
+    if (rc) return rc;
   }
-  if (dtype == SNRSE_F32) return dispatch_conv<float, float>(p, stream);
-  return SNRSE_EINVAL;
+  return 0;
 }
 
 #ifdef SNRSE_STAMPS
@@ -1669,8 +1453,7 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   if (!name || !value) return SNRSE_EINVAL;
   if (name_is(name, "conv_variant")) { *value = g_conv_variant; return 0; }
   if (name_is(name, "halo_kernel")) {  // generation taken by a halo-eligible bf16 conv
-    const int v = g_conv_variant == 0 ? kHaloAuto : g_conv_variant;
-    *value = (v == 8 || v == 6 || v == 5) ? v : 4;
+    *value = kHaloAuto;
     return 0;
   }
   if (name_is(name, "last_kernel")) { *value = g_last_kernel; return 0; }
@@ -1680,6 +1463,8 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   if (name_is(name, "h5_stagger")) { *value = g_h5_stagger_per_phase; return 0; }
   if (name_is(name, "stats_zeroed")) { *value = g_snrse_stats_zeroed; return 0; }
   if (name_is(name, "last_ksplit")) { *value = g_last_ksplit; return 0; }
+  if (name_is(name, "last_epi_nt")) { *value = g_last_epi_nt; return 0; }
+  if (name_is(name, "last_chunks")) { *value = g_last_chunks; return 0; }
   return SNRSE_EINVAL;
 }
 

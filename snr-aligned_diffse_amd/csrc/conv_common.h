@@ -1,5 +1,5 @@
 // Shared parameter block and device helpers of the implicit-GEMM conv kernels
-// (conv.hip: v1/v2/v4/v5 kernels + C-ABI; conv_halo6.hip: persistent halo GEMM).
+// (conv.hip: v1/v2/v5 kernels + C-ABI; conv_head.hip: pyramid heads).
 #pragma once
 #include "common.h"
 
@@ -92,13 +92,6 @@ SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
 }
 
-// Persistent halo GEMM (conv_halo6.hip).  Returns a hipError_t (0 = launched) or
-// SNRSE_EINVAL when the shape / operands are outside its contract.
-int launch_halo6(const ConvParams& p, hipStream_t s);
-bool halo6_ok(const ConvParams& p);
-// 8-wave ping-pong halo GEMM (conv_halo8.hip): ResBlock convs without shortcut / Combine, H % 8 == 0.
-int launch_halo8(const ConvParams& p, hipStream_t s);
-bool halo8_ok(const ConvParams& p);
 // Pyramid heads (conv_head.hip): 3x3, Cout <= 16, f32 output, optional fused GroupNorm+SiLU.
 int launch_head(const ConvParams& p, hipStream_t s);
 bool head_ok(const ConvParams& p);

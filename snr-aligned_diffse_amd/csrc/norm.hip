@@ -193,7 +193,17 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const Tin* src0, int C0, 
 
 // Generic upfirdn2d on [major, in_h, in_w, minor] (the reference op's layout):
 // out[y, x] = sum_{i,j} k[kh-1-i][kw-1-j] * up_pad(in)[y*dy + i][x*dx + j]
-template <typename T>
+// Element types of the reference binding (AT_DISPATCH_FLOATING_TYPES_AND_HALF, upfirdn2d_kernel.cu:311)
+// plus bf16: f32 / bf16 / f16 accumulate in f32, f64 in f64.
+SNRSE_DEV float ufd_ld(float v) { return v; }
+SNRSE_DEV float ufd_ld(bf16_t v) { return bf2f(v); }
+SNRSE_DEV float ufd_ld(_Float16 v) { return (float)v; }
+SNRSE_DEV double ufd_ld(double v) { return v; }
+template <typename T> SNRSE_DEV T ufd_st(float v) { return (T)v; }
+template <> SNRSE_DEV bf16_t ufd_st<bf16_t>(float v) { return f2bf(v); }
+template <typename T> SNRSE_DEV T ufd_st(double v) { return (T)v; }
+
+template <typename T, typename A>
 __global__ void upfirdn2d_kernel(const T* in, T* out, const float* kern, int major, int in_h, int in_w,
                                  int minor, int kh, int kw, int up_x, int up_y, int down_x, int down_y,
                                  int pad_x0, int pad_y0, int out_h, int out_w) {
@@ -205,7 +215,7 @@ __global__ void upfirdn2d_kernel(const T* in, T* out, const float* kern, int maj
     const int ox = r % out_w; r /= out_w;
     const int oy = r % out_h;
     const int mj = (int)(r / out_h);
-    float acc = 0.f;
+    A acc = 0;
     for (int i = 0; i < kh; ++i) {
       const int uy = oy * down_y + i - pad_y0;  // coordinate in the upsampled grid
       if (uy < 0 || uy % up_y) continue;
@@ -216,11 +226,10 @@ __global__ void upfirdn2d_kernel(const T* in, T* out, const float* kern, int maj
         if (ux < 0 || ux % up_x) continue;
         const int ix = ux / up_x;
         if (ix >= in_w) continue;
-        acc += kern[(kh - 1 - i) * kw + (kw - 1 - j)] *
-               Elem<T>::to_f(in[(((size_t)mj * in_h + iy) * in_w + ix) * minor + mi]);
+        acc += (A)kern[(kh - 1 - i) * kw + (kw - 1 - j)] * (A)ufd_ld(in[(((size_t)mj * in_h + iy) * in_w + ix) * minor + mi]);
       }
     }
-    out[idx] = Elem<T>::from_f(acc);
+    out[idx] = ufd_st<T>(acc);
   }
 }
 
@@ -342,15 +351,14 @@ extern "C" int snrse_upfirdn2d(const void* in, void* out, const float* kernel, i
   const size_t total = (size_t)major * out_h * out_w * minor;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 65536) blocks = 65536;
-  if (dtype == SNRSE_F32)
-    hipLaunchKernelGGL(upfirdn2d_kernel<float>, dim3(blocks), dim3(256), 0, stream, (const float*)in,
-                       (float*)out, kernel, major, in_h, in_w, minor, kh, kw, up_x, up_y, down_x, down_y,
-                       pad_x0, pad_y0, out_h, out_w);
-  else if (dtype == SNRSE_BF16)
-    hipLaunchKernelGGL(upfirdn2d_kernel<bf16_t>, dim3(blocks), dim3(256), 0, stream, (const bf16_t*)in,
-                       (bf16_t*)out, kernel, major, in_h, in_w, minor, kh, kw, up_x, up_y, down_x, down_y,
-                       pad_x0, pad_y0, out_h, out_w);
-  else
-    return SNRSE_EINVAL;
+#define SNRSE_UFD(T, A)                                                                                      \
+  hipLaunchKernelGGL((upfirdn2d_kernel<T, A>), dim3(blocks), dim3(256), 0, stream, (const T*)in, (T*)out, kernel, \
+                     major, in_h, in_w, minor, kh, kw, up_x, up_y, down_x, down_y, pad_x0, pad_y0, out_h, out_w)
+  if (dtype == SNRSE_F32) SNRSE_UFD(float, float);
+  else if (dtype == SNRSE_BF16) SNRSE_UFD(bf16_t, float);
+  else if (dtype == SNRSE_F16) SNRSE_UFD(_Float16, float);
+  else if (dtype == SNRSE_F64) SNRSE_UFD(double, double);
+  else return SNRSE_EINVAL;
+#undef SNRSE_UFD
   return (int)hipGetLastError();
 }

@@ -19,6 +19,8 @@
 //                      z is read from a tensor (parity mode) or drawn in-kernel (Philox4x32-10).
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr float kTwoPi = 6.28318530717958647692f;
@@ -421,10 +423,17 @@ extern "C" int snrse_temb_mlp(const float* t, const float* Wg, const float* W1, 
 
 extern "C" int snrse_temb_dense(const float* temb, const float* W, const float* bias, float* out, int B, int R,
                                 int D, hipStream_t s) {
-  if (D > 512 || D % 4 || B <= 0 || B > 32 || (size_t)B * D * 4 > 64 * 1024) return SNRSE_EINVAL;
-  hipLaunchKernelGGL(temb_dense_kernel, dim3((R + 63) / 64), dim3(256), sizeof(float) * B * D, s, temb, W, bias,
-                     out, B, R, D);
-  return (int)hipGetLastError();
+  if (D > 512 || D % 4 || B <= 0 || R <= 0) return SNRSE_EINVAL;
+  // the kernel stages a [b][D] table of SiLU(temb) in LDS: launch over batch chunks of at most 32
+  // utterances (64 KB at D = 512) so any batch size works
+  const int chunk = std::max(1, std::min(32, (64 * 1024) / (4 * D)));
+  for (int b0 = 0; b0 < B; b0 += chunk) {
+    const int nb = std::min(chunk, B - b0);
+    hipLaunchKernelGGL(temb_dense_kernel, dim3((R + 63) / 64), dim3(256), sizeof(float) * nb * D, s,
+                       temb + (size_t)b0 * D, W, bias, out + (size_t)b0 * R, nb, R, D);
+    SNRSE_LAUNCH_CHECK();
+  }
+  return 0;
 }
 
 extern "C" int snrse_input_conv(const void* x, const void* y, int B, int H, int W, const void* wgt, const float* bias,

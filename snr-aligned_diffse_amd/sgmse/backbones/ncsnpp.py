@@ -86,6 +86,7 @@ class NCSNpp(nn.Module):
                 raise NotImplementedError(f"NCSNpp option {k}={v!r} is not built for the HIP path")
         self.cfg = dict(nf=nf, ch_mult=tuple(ch_mult), num_res_blocks=num_res_blocks,
                         attn_resolutions=tuple(attn_resolutions), image_size=image_size)
+        _hip.check_topology(**self.cfg)  # the executor is built for the shipped topology only
         self.compute_dtype = compute_dtype
         self.output_layer = nn.Conv2d(4, 2, 1)
         mods = []

@@ -74,8 +74,10 @@ class Specs(torch.utils.data.Dataset):
         y, _ = audio.load(self.noisy_files[i])
         return x, y
 
-    def _specs(self, xs, ys, fixed_snr):
-        """Device half for stacked host crops xs, ys [B, L] -> (X, Y) [B, 1, 256, num_frames]."""
+    def _specs(self, xs, ys, fixed_snr, one_clip=False):
+        """Device half for stacked host crops xs, ys [B, L] -> (X, Y) [B, 1, 256, num_frames].
+        one_clip: the rows are the C channels of ONE clip, normalised by one max over all of them
+        (y.abs().max(), data_module.py:70-75) instead of per row."""
         dev = _device()
         B = xs.shape[0]
         xy = torch.cat([xs, ys], 0).to(dev, torch.float32, non_blocking=True)
@@ -90,6 +92,8 @@ class Specs(torch.utils.data.Dataset):
             nf = None
         else:
             raise ValueError(f"normalize {self.normalize!r}")
+        if one_clip and nf is not None and B > 1:
+            nf = nf.max().reshape(1).expand(B).contiguous()
         fused = getattr(self.spec_transform, "__func__", None) is SpecsDataModule.spec_fwd and \
             self.spec_transform.__self__.transform_type == "exponent"
         mode = 1 if fused else 0
@@ -102,8 +106,8 @@ class Specs(torch.utils.data.Dataset):
     def __getitem__(self, i):
         x, y = self._load_pair(i)
         x, y = self._crop(x, y)
-        X, Y = self._specs(x, y, self.fixed_snr)
-        return X[0], Y[0]
+        X, Y = self._specs(x, y, self.fixed_snr, one_clip=True)
+        return X[:, 0], Y[:, 0]  # [C, F, T] like torch.stft of a [C, L] clip
 
     def batch(self, indices):
         """(X, Y) [len(indices), 1, 256, num_frames] for a list of clip indices, one device pass
@@ -186,6 +190,13 @@ class SpecsDataModule:
             raise NotImplementedError("the HIP transform is built for exponent 0.5, factor 0.15")
         if self.transform_type not in ("exponent", "none"):
             raise NotImplementedError(f"transform_type {self.transform_type} is not built for the HIP path")
+
+    def hip_mode(self):
+        """Spectrogram mode of the fused HIP STFT / iSTFT for this configuration: 1 = 'exponent'
+        transform fused (spec_fwd / spec_back, data_module.py:241-267), 0 = raw ('none').  Raises for a
+        configuration the kernels are not built for (_check)."""
+        self._check()
+        return 1 if self.transform_type == "exponent" else 0
 
     def setup(self, stage=None):
         """Datasets of data_module.py:221-240 (device-producing Specs / Specs_SNR)."""

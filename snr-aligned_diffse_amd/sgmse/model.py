@@ -230,6 +230,9 @@ class ScoreModel(nn.Module):
                 corrector_steps=1, snr=0.5, timeit=False, oracle=False, clean_rms=1, noise_rms=1, **kwargs):
         """One-call enhancement of noisy speech y [1, L] (model.py:702-839) -> numpy [L]."""
         start = time.time()
+        # the checkpoint's data-module hparams pick the front / back end (_forward_transform(_stft(.)),
+        # model.py:749, to_audio 612-613): fused exponent transform or raw, anything else raises
+        mode = self.data_module.hip_mode()
         dev = torch.device("cuda", torch.cuda.current_device())
         T_orig = y.size(1)
         yd = y.to(dev, torch.float32).reshape(1, -1).contiguous()
@@ -252,7 +255,7 @@ class ScoreModel(nn.Module):
             t_hat = float(t_30[np.abs(t_30 - est_snr / (10 ** 0.25 * self.fixed_snr)).argmin()])
             normfac = self.calculate_normfac_direct(1.0, 10 ** 0.25 * self.fixed_snr * t_hat, self.fixed_snr)
             div = nf * float(normfac)
-            Y = ops.stft(yd, 1.0, tpad=Tp, mode=1, in_div=div)
+            Y = ops.stft(yd, 1.0, tpad=Tp, mode=mode, in_div=div)
             z_scale = float(self.sigma_max) * t_hat
             Z = noise_tape(0) if noise_tape is not None else None
             coef = torch.tensor([[0.0, 1.0, 0.0, z_scale]], device=dev)
@@ -261,7 +264,7 @@ class ScoreModel(nn.Module):
             out_scale = div
         else:
             div = nf
-            Y = ops.stft(yd, 1.0, tpad=Tp, mode=1, in_div=div)
+            Y = ops.stft(yd, 1.0, tpad=Tp, mode=mode, in_div=div)
             if self.model_type == "bbed":
                 if sampler_type == "pc":
                     sampler = self.get_pc_sampler(predictor, corrector, Y[:, None], N=N, corrector_steps=corrector_steps,
@@ -282,7 +285,7 @@ class ScoreModel(nn.Module):
             else:
                 raise NotImplementedError(f"model_type={self.model_type!r} with snr_conditioned='false'")
             out_scale = div
-        x_hat = ops.istft(sample.contiguous(), T_orig, mode=1, out_scale=out_scale.reshape(1).contiguous())
+        x_hat = ops.istft(sample.contiguous(), T_orig, mode=mode, out_scale=out_scale.reshape(1).contiguous())
         x_hat = x_hat[0].cpu().numpy()
         if timeit:
             rtf = (time.time() - start) / (len(x_hat) / 16000)

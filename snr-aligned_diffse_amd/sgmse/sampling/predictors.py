@@ -19,6 +19,8 @@ class Predictor(abc.ABC):
     def __init__(self, sde, score_fn, probability_flow=False):
         super().__init__()
         self.sde = sde
+        # as the reference (predictors.py:18): the reverse SDE is built WITHOUT probability_flow, so the
+        # flag is stored but changes nothing in the updates below
         self.rsde = sde.reverse(score_fn)
         self.score_fn = score_fn
         self.probability_flow = probability_flow
@@ -51,10 +53,8 @@ class EulerMaruyamaPredictor(Predictor):
         tt = float(t.reshape(-1)[0])
         dt = -1.0 / self.rsde.N
         kap, g = sp.drift_coef(tt), sp.g(tt)
-        pf = 0.5 if self.probability_flow else 1.0
         score = self.score_fn(x, t, y)
-        return self._step(x, y, score, 1.0 - kap * dt, kap * dt, -pf * g * g * dt,
-                          0.0 if self.probability_flow else g * math.sqrt(-dt))
+        return self._step(x, y, score, 1.0 - kap * dt, kap * dt, -g * g * dt, g * math.sqrt(-dt))
 
 
 @PredictorRegistry.register("reverse_diffusion")
@@ -66,9 +66,8 @@ class ReverseDiffusionPredictor(Predictor):
         st = float(stepsize)
         kap = sp.drift_coef(tt)
         G = sp.g(tt) * math.sqrt(st)
-        pf = 0.5 if self.probability_flow else 1.0
         score = self.score_fn(x, t, y)
-        return self._step(x, y, score, 1.0 + kap * st, -kap * st, pf * G * G, 0.0 if self.probability_flow else G)
+        return self._step(x, y, score, 1.0 + kap * st, -kap * st, G * G, G)
 
 
 @PredictorRegistry.register("none")

@@ -117,9 +117,9 @@ class OUVESDE(SDE):
         self._T = 1
 
     def copy(self):
-        c = OUVESDE(self.theta, self.sigma_min, self.sigma_max, N=self.N)
-        c._T = self._T
-        return c
+        # as the reference (sdes.py:185-186): the copy starts from the constructor's _T = 1, so
+        # eval.py's `model.sde._T = reverse_starting_point` does not reach get_pc_sampler (model.py:552)
+        return OUVESDE(self.theta, self.sigma_min, self.sigma_max, N=self.N)
 
     @property
     def T(self):

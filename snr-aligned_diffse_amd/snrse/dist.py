@@ -63,3 +63,47 @@ def gather_metrics(values, n_total: int, rank: int, world: int, device):
         a, b = shard_range(n_total, r, world)
         rows.append(bufs[r][: b - a])
     return torch.cat(rows, 0)
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_entry(rank, world, port, fn, args):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    fn(*args)
+
+
+def spawn_ranks(world: int, fn, args=(), poll_s: float = 0.5) -> int:
+    """Run fn(*args) in `world` fresh processes (multiprocessing 'spawn'), rank r on GPU r, with
+    torchrun's environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT).
+    The caller must not have initialised the GPU (children are new interpreters, nothing is exec'd
+    over a GPU-initialised process).  If a rank fails, the others are terminated instead of being
+    left waiting in a collective.  Returns 0 or the first failing rank's exit code."""
+    import time
+
+    import torch.multiprocessing as mp
+    port = free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_rank_entry, args=(r, world, port, fn, args)) for r in range(world)]
+    for p in procs:
+        p.start()
+    rc = 0
+    while any(p.is_alive() for p in procs):
+        bad = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            for p in procs:
+                if p.is_alive():
+                    p.terminate()
+            break
+        time.sleep(poll_s)
+    for p in procs:
+        p.join()
+        if rc == 0 and p.exitcode:
+            rc = p.exitcode
+    return rc

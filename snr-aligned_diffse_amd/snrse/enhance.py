@@ -38,12 +38,22 @@ def pad_frames(T, mult=64):
     return T + ((mult - T % mult) % mult)
 
 
+TRANSFORM_MODES = {"exponent": 1, "none": 0}  # fused spec_fwd/spec_back (|c|^0.5 e^{i angle} 0.15) or raw
+
+
+def transform_mode(transform):
+    if transform not in TRANSFORM_MODES:
+        raise NotImplementedError(f"transform_type {transform!r} is not built for the HIP path")
+    return TRANSFORM_MODES[transform]
+
+
 class PCEnhancer:
     """PC-sampler enhancement of a batch of noisy waveforms with an NCSNppHIP network."""
 
     def __init__(self, net, sde: sampler.SDESpec, N=30, eps=0.03, snr=0.5, predictor="reverse_diffusion",
-                 corrector="ald", corrector_steps=1, score_mode=0):
+                 corrector="ald", corrector_steps=1, score_mode=0, transform="exponent"):
         self.net, self.sde, self.N, self.eps, self.snr = net, sde, N, eps, snr
+        self.mode = transform_mode(transform)
         self.predictor, self.corrector, self.corrector_steps = predictor, corrector, corrector_steps
         self.score_mode = score_mode
 
@@ -68,9 +78,9 @@ class PCEnhancer:
         B, L = y.shape
         nf = ops.absmax(y)  # norm_factor = max|y| (model.py:726)
         T = 1 + L // 128
-        Y = ops.stft(y, 1.0, tpad=pad_frames(T), mode=1, in_div=nf)
+        Y = ops.stft(y, 1.0, tpad=pad_frames(T), mode=self.mode, in_div=nf)
         x, nfe = self.sample(Y, noise)
-        return ops.istft(x, L, mode=1, out_scale=nf), nfe
+        return ops.istft(x, L, mode=self.mode, out_scale=nf), nfe
 
 
 class SNRAlignedEnhancer:
@@ -83,8 +93,9 @@ class SNRAlignedEnhancer:
     max|y| normfac.  The per-utterance scalars (t_hat, normfac) are host float64 as in the
     reference (one B-element copy).  Returns (x_hat [B, L], t_hat numpy [B])."""
 
-    def __init__(self, net, snr_fn=None, fixed_snr=0.17783, sigma_max=0.5):
+    def __init__(self, net, snr_fn=None, fixed_snr=0.17783, sigma_max=0.5, transform="exponent"):
         self.net, self.snr_fn = net, snr_fn
+        self.mode = transform_mode(transform)
         self.fixed_snr, self.sigma_max = float(fixed_snr), float(sigma_max)
 
     def __call__(self, y, est_snr=None, noise=None, seed=0):
@@ -96,11 +107,11 @@ class SNRAlignedEnhancer:
             est_snr = self.snr_fn(raw).reshape(B).double().cpu().numpy()
         t_hat = snap_t(est_snr, self.fixed_snr)
         div = nf * torch.from_numpy(normfac(t_hat, self.fixed_snr)).to(nf.device, torch.float32)
-        Y = ops.stft(y, 1.0, tpad=pad_frames(1 + L // 128), mode=1, in_div=div)
+        Y = ops.stft(y, 1.0, tpad=pad_frames(1 + L // 128), mode=self.mode, in_div=div)
         coef = torch.zeros(B, 4, dtype=torch.float32)
         coef[:, 1] = 1.0
         coef[:, 3] = torch.from_numpy(self.sigma_max * t_hat).float()
         X_T = ops.axpby_noise(coef.to(Y.device), y=Y, noise=noise, seed=seed)
         tv = torch.from_numpy(t_hat).to(Y.device, torch.float32)
         sample = self.net.score(X_T, Y, tv, 1)
-        return ops.istft(sample.contiguous(), L, mode=1, out_scale=div.contiguous()), t_hat
+        return ops.istft(sample.contiguous(), L, mode=self.mode, out_scale=div.contiguous()), t_hat

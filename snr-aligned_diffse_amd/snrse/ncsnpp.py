@@ -86,6 +86,20 @@ def build_plan(nf=128, ch_mult=(1, 1, 2, 2, 2, 2, 2), num_res_blocks=2, attn_res
     return mods
 
 
+SHIPPED = dict(nf=128, ch_mult=(1, 1, 2, 2, 2, 2, 2), num_res_blocks=2, attn_resolutions=(16,), image_size=256)
+
+
+def check_topology(**cfg):
+    """The executor (_pyramid) hard-codes the shipped NCSN++ topology (ncsnpp.py:45-245 with the
+    defaults of the README configuration): reject any other one at construction instead of
+    mis-executing a checkpoint."""
+    for k, v in cfg.items():
+        want = SHIPPED.get(k)
+        got = tuple(v) if isinstance(v, (list, tuple)) else v
+        if want is not None and got != want:
+            raise NotImplementedError(f"NCSNpp {k}={v!r}: the HIP executor is built for {k}={want!r} only")
+
+
 def _pack3x3(w, dt, npad=None):
     co = w.shape[0]
     p = w.permute(0, 2, 3, 1).reshape(co, -1)
@@ -107,6 +121,7 @@ class NCSNppHIP:
         self.dtype = dtype
         self.device = torch.device(device)
         self._arena = None  # ops.StatsArena of the GroupNorm statistics, one fill per evaluation
+        check_topology(**cfg)
         self.plan = build_plan(**cfg)
         dev, dt = self.device, dtype
         f32 = lambda k: sd[k].detach().to(dev, torch.float32).contiguous()  # noqa: E731

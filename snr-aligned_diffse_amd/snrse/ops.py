@@ -1,6 +1,12 @@
 """Torch-tensor wrappers over the C-ABI (device pointers + torch's current stream).
 
 Every op requires HIP device tensors and raises otherwise — there is no CPU fallback.
+
+Concurrency contract: ONE stream per process runs network evaluations.  Two pieces of state are
+process-wide and ordered only by that stream: the split-K workspace (_WS / the library's g_ws) and
+each network's StatsArena (zeroed on the current stream when an evaluation starts).  Running two
+evaluations concurrently on different streams would race on both; the multi-GPU path uses one
+process per GPU, so it never does.
 """
 from __future__ import annotations
 
@@ -89,8 +95,7 @@ def get_option(name):
     return v.value
 
 
-KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 4: "conv_halo_kernel", 5: "conv_halo5_kernel",
-           6: "conv_halo6_kernel", 8: "conv_halo8_kernel", 9: "conv_head_kernel"}
+KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 5: "conv_halo5_kernel", 9: "conv_head_kernel"}
 
 
 def kernel_name(gen):
@@ -104,18 +109,18 @@ def conv_kernel_name():
 
 
 def halo_ok(x, ksize, cout):
-    """True when snrse_conv2d takes the halo path (and so accepts a fused GroupNorm)."""
+    """True when snrse_conv2d takes the halo path (and so accepts a fused GroupNorm).  Any batch size
+    qualifies: sources beyond 2 GiB run as consecutive launches over image ranges (snrse_conv2d)."""
     B, H, W, C = x.shape
     return (x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and H % 4 == 0 and W % 64 == 0
-            and _VARIANT["v"] in (0, 4, 5, 6, 8) and x.numel() * 2 < 0x7ff00000)
+            and _VARIANT["v"] in (0, 5))
 
 
 def head_ok(x):
     """True when a bf16 3x3 conv of x with Cout <= 16 and f32 output (the pyramid heads) takes the
     halo-staged head kernel, which accepts a fused GroupNorm (gn=)."""
     B, H, W, C = x.shape
-    return (x.dtype == torch.bfloat16 and H % 4 == 0 and W % 64 == 0 and C % 32 == 0 and _VARIANT["v"] != 1
-            and x.numel() * 2 < 0x7ff00000)
+    return x.dtype == torch.bfloat16 and H % 4 == 0 and W % 64 == 0 and C % 32 == 0 and _VARIANT["v"] != 1
 
 
 def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):
@@ -430,6 +435,9 @@ def istft(spec, length, mode=1, out_scale=None):
     return out
 
 
+UPFIRDN_DTYPES = {torch.float32: F32, torch.bfloat16: BF16, torch.float16: _lib.F16, torch.float64: _lib.F64}
+
+
 def upfirdn2d(inp, kernel, up=1, down=1, pad=(0, 0)):
     """Reference-signature upfirdn2d (op/upfirdn2d.py:145-156) on [N, C, H, W]."""
     _dev(inp, kernel)
@@ -440,8 +448,11 @@ def upfirdn2d(inp, kernel, up=1, down=1, pad=(0, 0)):
     ow = (W * up + pad[0] + pad[1] - kw) // down + 1
     out = torch.empty(N * Cc, oh, ow, 1, device=inp.device, dtype=inp.dtype)
     k = kernel.to(torch.float32).contiguous()
+    dt = UPFIRDN_DTYPES.get(inp.dtype)
+    if dt is None:
+        raise TypeError(f"upfirdn2d: unsupported dtype {inp.dtype} (float, double, half, bfloat16)")
     _lib.call("snrse_upfirdn2d", x.data_ptr(), out.data_ptr(), k.data_ptr(), N * Cc, H, W, 1, kh, kw, up, up,
-              down, down, pad[0], pad[1], pad[0], pad[1], code(inp.dtype), _stream())
+              down, down, pad[0], pad[1], pad[0], pad[1], dt, _stream())
     return out.view(N, Cc, oh, ow)
 
 

@@ -74,7 +74,9 @@ def timesteps(T, N, eps):
 
 
 def build_schedule(sde: SDESpec, N, eps, predictor, corrector, snr, corrector_steps, probability_flow=False):
-    """List of ('corr'|'pred', t, (a, by, c, s)) in execution order + prior coefficient."""
+    """List of ('corr'|'pred', t, (a, by, c, s)) in execution order + prior coefficient.
+    `probability_flow` is accepted and ignored, as in the reference: its Predictor builds the reverse
+    SDE without the flag (predictors.py:18), so the PC updates never change with it."""
     ts = timesteps(sde.T, N, eps)
     steps = []
     for i in range(N):
@@ -90,16 +92,13 @@ def build_schedule(sde: SDESpec, N, eps, predictor, corrector, snr, corrector_st
         elif corrector != "none":
             raise ValueError(f"Corrector with name '{corrector}' unknown.")
         kap = sde.drift_coef(t)
-        pf = 0.5 if probability_flow else 1.0
         if predictor == "reverse_diffusion":
             G = sde.g(t) * math.sqrt(stepsize)
-            steps.append(("pred", t, (1.0 + kap * stepsize, -kap * stepsize, pf * G * G,
-                                      0.0 if probability_flow else G)))
+            steps.append(("pred", t, (1.0 + kap * stepsize, -kap * stepsize, G * G, G)))
         elif predictor == "euler_maruyama":
             dt = -1.0 / N
             g = sde.g(t)
-            steps.append(("pred", t, (1.0 - kap * dt, kap * dt, -pf * g * g * dt,
-                                      0.0 if probability_flow else g * math.sqrt(-dt))))
+            steps.append(("pred", t, (1.0 - kap * dt, kap * dt, -g * g * dt, g * math.sqrt(-dt))))
         elif predictor == "none":
             steps.append(("none", t, None))
         else:

@@ -114,3 +114,30 @@ def test_gloo_world2_evaluate_sharded(tmp_path):
     assert sir0 == [0.0, 0.0, 0.0, 1.0, 1.0]        # which rank scored each file
     lines = open(os.path.join(out, "_results.csv")).read().splitlines()
     assert len(lines) == 6 and lines[1].startswith("u0.wav,nan,1000.0,0.0,")
+
+
+def _spawned_child(path):
+    """What bench.py's --gpus N launcher runs per rank, on gloo: init from the env it was given."""
+    from snrse import dist as sd
+    r, w, dev = sd.init_from_env("gloo")
+    t = sd.max_over_ranks(0.5 * (r + 1), dev)
+    allm = sd.gather_metrics([[float(r)]] * 3, 3 * w, r, w, dev)
+    if r == 0:
+        with open(path, "w") as f:
+            f.write(f"{w} {t} {allm[:, 0].tolist()}")
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def _failing_child():
+    raise SystemExit(3)
+
+
+def test_spawn_ranks_world2(tmp_path):
+    """snrse.dist.spawn_ranks -- the launcher behind `bench.py --gpus N` -- starts N ranks with the
+    torchrun environment; a failing rank's code is returned."""
+    from snrse import dist as sd
+    path = str(tmp_path / "r0.txt")
+    assert sd.spawn_ranks(2, _spawned_child, (path,)) == 0
+    assert open(path).read() == "2 1.0 [0.0, 0.0, 0.0, 1.0, 1.0, 1.0]"
+    assert sd.spawn_ranks(2, _failing_child) == 3

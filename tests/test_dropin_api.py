@@ -95,3 +95,63 @@ def test_checkpoint_roundtrip_with_ema(tmp_path):
     assert torch.equal(m.dnn.all_modules[0].W, sd["dnn.all_modules.0.W"])  # frozen GFP not in EMA
     m.train()
     assert torch.equal(w, sd["dnn.all_modules.4.Conv_0.weight"])
+
+
+def test_ouve_copy_resets_starting_point():
+    """OUVESDE.copy() starts from _T = 1 like the reference (sdes.py:185-186), so eval.py's
+    `model.sde._T = reverse_starting_point` (eval.py:105-108) never reaches the PC sampler, which
+    always samples from a copy (model.py:552): the schedule starts at t = 1."""
+    from sgmse.sdes import OUVESDE
+    from snrse import sampler
+    sde = OUVESDE(theta=1.5, sigma_min=0.05, sigma_max=0.5, N=30)
+    sde._T = 0.5  # eval.py --reverse_starting_point 0.5
+    c = sde.copy()
+    assert sde.T == 0.5 and c.T == 1 and c.N == 30
+    steps, prior, _ = sampler.build_schedule(c.spec(), 15, 0.03, "reverse_diffusion", "ald", 0.5, 1)
+    assert steps[0][1] == 1.0
+    assert abs(prior[3] - sampler.SDESpec("ouve", theta=1.5, sigma_min=0.05, sigma_max=0.5).std(1.0)) < 1e-12
+
+
+def test_unsupported_topology_rejected_at_construction():
+    from sgmse.backbones import BackboneRegistry
+    cls = BackboneRegistry.get_by_name("ncsnpp")
+    cls()  # the shipped topology constructs
+    for kw in (dict(nf=64), dict(ch_mult=(1, 2, 2, 2)), dict(num_res_blocks=4), dict(attn_resolutions=(8,)),
+               dict(image_size=128)):
+        with pytest.raises(NotImplementedError):
+            cls(**kw)
+
+
+def test_probability_flow_does_not_change_pc_schedule():
+    """The reference's Predictor builds rsde without probability_flow (predictors.py:18): the flag
+    changes nothing in the PC updates."""
+    from snrse import sampler
+    sde = sampler.SDESpec("ouve", theta=1.5, sigma_min=0.05, sigma_max=0.5)
+    for pred in ("reverse_diffusion", "euler_maruyama"):
+        a = sampler.build_schedule(sde, 7, 0.03, pred, "ald", 0.5, 1, probability_flow=False)
+        b = sampler.build_schedule(sde, 7, 0.03, pred, "ald", 0.5, 1, probability_flow=True)
+        assert a == b
+
+
+def test_enhance_follows_data_module_transform():
+    """enhance() takes its front / back end from the checkpoint's data-module hparams
+    (model.py:749, 612-613): 'exponent' -> fused mode 1, 'none' -> raw mode 0, a configuration the
+    HIP kernels are not built for raises before any device work."""
+    from sgmse.data_module import SpecsDataModule
+    from sgmse.model import ScoreModel
+    assert SpecsDataModule().hip_mode() == 1
+    assert SpecsDataModule(transform_type="none").hip_mode() == 0
+    for kw in (dict(window="sqrthann"), dict(spec_factor=0.3), dict(transform_type="log")):
+        with pytest.raises(NotImplementedError):
+            SpecsDataModule(**kw).hip_mode()
+    m = ScoreModel(backbone="ncsnpp", sde="ouve", model_type="bbed", theta=1.5, sigma_min=0.05, sigma_max=0.5,
+                   window="sqrthann")
+    with pytest.raises(NotImplementedError):
+        m.enhance(torch.zeros(1, 1000), torch.zeros(1, 1000))
+
+
+def test_upfirdn2d_dtype_table():
+    """The reference binding dispatches float / double / half (upfirdn2d_kernel.cu:311)."""
+    from snrse import _lib, ops
+    assert set(ops.UPFIRDN_DTYPES) == {torch.float32, torch.float64, torch.float16, torch.bfloat16}
+    assert (_lib.F16, _lib.F64) == (2, 3)

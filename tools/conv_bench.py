@@ -65,7 +65,7 @@ def run(shape, variant, reps, dev, gn=False):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--variants", default="4,5,6")
+    ap.add_argument("--variants", default="5")
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--shapes", default="", help="comma list of SHAPES indices (default all)")
     ap.add_argument("--gn", action="store_true", help="fused GroupNorm+SiLU prologue (halo kernels)")

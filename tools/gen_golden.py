@@ -35,8 +35,14 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference/sgmse-bbed"
 OUT = os.path.join(REPO, "tests", "golden")
 
-sys.path.insert(0, os.path.join(REPO, "snr-aligned_diffse_amd"))
-from snrse import formula  # noqa: E402
+# snrse/formula.py is loaded by file path: putting the build's package directory on sys.path would
+# let its regular `sgmse` package shadow the reference's namespace package of the same name.
+import importlib.util  # noqa: E402
+
+_spec = importlib.util.spec_from_file_location(
+    "snrse_formula", os.path.join(REPO, "snr-aligned_diffse_amd", "snrse", "formula.py"))
+formula = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(formula)
 
 os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
 sys.dont_write_bytecode = True
@@ -333,14 +339,75 @@ def gen_sebridge_enhance():
     save("enhance_inputs.npz", noisy_valid_i16=noisy)
 
 
+C4_FILES = ["VBD_SNR-5/valid/noisy/p232_001.wav", "VBD_SNR-5/train2/noisy/p286_001.wav",
+            "VBD/train/noisy/p226_001.wav"]
+C4_LEN = 27861
+C4_FC_BIAS_SHIFT = 2.1
+
+
+def pad_spec_16_ref(Y):  # util/other.py:92-99
+    return pad_spec_ref(Y, 16)
+
+
+def gen_snr_enhance():
+    """C4: ScoreModel.enhance, sebridge_v3, snr_conditioned='true', oracle=False -- the SNR comes from
+    the reference SNRNet on the raw STFT (model.py:713-721), then t_hat / normfac / noise / one
+    preconditioned NCSNpp evaluation / iSTFT as model.py:726-833.  Three dataset utterances cropped to
+    one length (so the GPU test can also run them as one batch), each processed at B=1 as the
+    reference does; noise draw k is formula noise golden.c4.Z.{k}."""
+    net = BackboneRegistry.get_by_name("ncsnpp")().eval()
+    load_formula(net)
+    snr_net = SNRNet().eval()
+    load_formula(snr_net, "snrnet.")
+    # formula weights put every clip's estimate at ~0.4 (t_hat snaps to 1.0 for all); shifting the
+    # output bias moves the estimates into the middle of the t_30 grid so the clips get distinct t_hat
+    with torch.no_grad():
+        snr_net.fc.bias -= C4_FC_BIAS_SHIFT
+    fixed_snr, sigma_max = 0.17783, 0.5
+    out = {"noisy_i16": [], "x_hat": [], "t_hat": [], "est_snr": [], "est_gt": []}
+    for k, rel in enumerate(C4_FILES):
+        noisy = read_wav(f"/root/reference/dataset/{rel}")[:C4_LEN]
+        y = torch.from_numpy(noisy.astype(np.float32) / 32768.0)[None]
+        T_orig = y.size(1)
+        with torch.no_grad():
+            y_chk = y / y.abs().max().item()
+            Yc = torch.view_as_real(stft_ref(y_chk)).permute(0, 3, 1, 2)
+            Yc = pad_spec_16_ref(Yc)
+            est_gt = snr_net(Yc)
+            est_snr = est_gt / (1 - est_gt)
+        norm_factor = y.abs().max().item()
+        t_ = (est_snr / (10 ** 0.25 * fixed_snr)).numpy()
+        t_ = T_30[np.abs(T_30 - t_).argmin()]
+        est_snr_ = torch.FloatTensor([10 ** 0.25 * fixed_snr * t_])
+        normfac_ = (2.040166) * (0.240253 + 0.759747 * fixed_snr ** 2) ** 0.5 / ((1 + est_snr_ ** 2) ** 0.5)
+        norm_factor = norm_factor * normfac_
+        yn = y / norm_factor
+        Y = pad_spec_ref(torch.unsqueeze(spec_fwd_ref(stft_ref(yn)), 0))
+        vec_t = torch.ones(1, 1, 1, 1) * float(t_)
+        Z = fnormal(f"golden.c4.Z.{k}", tuple(Y.shape), complex_=True) * sigma_max * float(t_)
+        X_T = Y + Z
+        eps, sd = 0.001, 0.5
+        c_skip = sd ** 2 / ((vec_t - eps) ** 2 + sd ** 2)
+        c_out = (sd * (vec_t - eps)) / ((sd ** 2 + vec_t ** 2) ** 0.5)
+        with torch.no_grad():
+            sample = c_skip * X_T + c_out * net(torch.cat([X_T, Y], dim=1), vec_t.reshape(1))
+            x_hat = istft_ref(spec_back_ref(sample.squeeze()), T_orig) * norm_factor
+        out["noisy_i16"].append(noisy)
+        out["x_hat"].append(t2n(x_hat).reshape(-1))
+        out["t_hat"].append(float(t_))
+        out["est_snr"].append(float(est_snr.reshape(-1)[0]))
+        out["est_gt"].append(float(est_gt.reshape(-1)[0]))
+    save("enhance_snrnet_c4.npz", **{k: np.asarray(v) for k, v in out.items()})
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["keys", "fir", "blocks", "attn", "ncsnpp", "sde", "pc_ouve",
-                             "pc_variants", "stft", "snrnet", "sebridge"]
+                             "pc_variants", "stft", "snrnet", "sebridge", "c4"]
     table = {"keys": gen_keys, "fir": gen_fir, "blocks": gen_blocks, "attn": gen_attn,
              "ncsnpp": gen_ncsnpp, "sde": gen_sde, "pc_ouve": gen_pc_ouve,
              "pc_variants": gen_pc_variants, "stft": gen_stft, "snrnet": gen_snrnet,
-             "sebridge": gen_sebridge_enhance}
+             "sebridge": gen_sebridge_enhance, "c4": gen_snr_enhance}
     for w in which:
         torch.manual_seed(0)
         table[w]()
