@@ -33,13 +33,13 @@ def nchw(x):
 DT = {"f32": (torch.float32, 2e-6), "bf16": (torch.bfloat16, 1e-2)}
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 5])
+@pytest.mark.parametrize("variant", [0, 1, 2, 5, 7])
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 16), (1, 256, 128, 4, 8), (3, 128, 256, 5, 7), (2, 384, 256, 4, 4),
                                    (2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (1, 256, 256, 12, 64)])
 def test_conv3x3(gpu, dt, shape, variant):
-    """variant: 0 auto (halo GEMM v5 where H%4==0, W%64==0), 1 register-staged, 2 LDS-DMA im2col,
-    5 halo v5 forced (two workgroups per CU)."""
+    """variant: 0 auto (the default halo GEMM where H%4==0, W%64==0), 1 register-staged, 2 LDS-DMA
+    im2col, 5 halo v5 forced, 7 halo v7 forced (bf16 output; f32 falls back to v5 / v1)."""
     from snrse import ops
     dtype, tol = DT[dt]
     B, cin, cout, H, W = shape
@@ -62,7 +62,7 @@ def test_conv3x3(gpu, dt, shape, variant):
 
 
 @pytest.mark.parametrize("epi_nt", [2, 0, 1])
-@pytest.mark.parametrize("variant", [0, 5])
+@pytest.mark.parametrize("variant", [0, 5, 7])
 @pytest.mark.parametrize("hw", [(8, 8), (8, 64)])
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 def test_conv_epilogue_shortcut_temb_comb(gpu, dt, hw, variant, epi_nt):
@@ -97,7 +97,7 @@ def test_conv_epilogue_shortcut_temb_comb(gpu, dt, hw, variant, epi_nt):
                          sc_wgt=w2.reshape(cout, cin).to(gpu, dtype).contiguous(), temb=temb.to(gpu), temb_off=20,
                          out_scale=1 / math.sqrt(2), comb=nhwc(pyr).to(gpu), comb_w=cw.to(gpu), comb_b=cb.to(gpu),
                          stats=st)
-        halo = ops.get_option("last_kernel") == 5
+        halo = ops.get_option("last_kernel") in (5, 7)
         nt = ops.get_option("last_epi_nt")
     finally:
         ops.set_option("conv_variant", 0)
@@ -353,7 +353,7 @@ def test_philox_noise_statistics(gpu):
 
 
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (2, 256, 128, 4, 64)])
-@pytest.mark.parametrize("variant", [0, 5])
+@pytest.mark.parametrize("variant", [0, 5, 7])
 def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     """Halo GEMM consuming SiLU(GN(x)) from raw x + per-(b,c) scale/shift (+ raw 1x1 shortcut)."""
     from snrse import ops
@@ -391,8 +391,9 @@ def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     (8, 256, 0, 256, 64, 128, 0, 0, True, True, False, True),      # two Cout tiles per image
     (2, 256, 256, 256, 32, 64, 0, 0, False, False, True, False),   # cat input, no GN
 ])
-def test_conv_halo5_large(gpu, case):
-    """The default halo GEMM (v5) vs an fp32 torch reference on the GPU at multi-image sizes, with
+@pytest.mark.parametrize("variant", [5, 7])
+def test_conv_halo_large(gpu, case, variant):
+    """The halo GEMMs (v5, v7) vs an fp32 torch reference on the GPU at multi-image sizes, with
     the fused GroupNorm+SiLU prologue, cat inputs, the 1x1 shortcut, temb, residual and the
     per-channel output statistics."""
     from snrse import ops
@@ -428,9 +429,14 @@ def test_conv_halo5_large(gpu, case):
         ref = ref + res.float().permute(0, 3, 1, 2)
     ref = ref * scale
     st = ops.new_stats(B, Co) if use_st else None
-    out = ops.conv2d(x0, w.reshape(Co, -1).contiguous(), 3, Co, bias=bias, src1=x1, sc=xs0, sc1=xs1, sc_wgt=ws,
-                     temb=temb, temb_off=40, res=res, out_scale=scale, stats=st, gn=gn)
-    assert ops.kernel_name(ops.get_option("last_kernel")) == "conv_halo5_kernel"
+    ops.set_option("conv_variant", variant)
+    try:
+        out = ops.conv2d(x0, w.reshape(Co, -1).contiguous(), 3, Co, bias=bias, src1=x1, sc=xs0, sc1=xs1, sc_wgt=ws,
+                         temb=temb, temb_off=40, res=res, out_scale=scale, stats=st, gn=gn)
+        ran = ops.kernel_name(ops.get_option("last_kernel"))
+    finally:
+        ops.set_option("conv_variant", 0)
+    assert ran == f"conv_halo{variant}_kernel"
     got = out.float().permute(0, 3, 1, 2)
     assert rel(got, ref) < 1e-2
     if use_st:
