@@ -201,6 +201,60 @@ int snrse_snrnet(const void* spec, int B, int T, const float* w5, const float* b
                  float* out, hipStream_t stream);
 size_t snrse_snrnet_workspace(int B, int T);
 
+/* ---- Consistency-training step (ScoreModel._step, model.py:361-390, with the
+ * backward pass PyTorch Lightning runs through loss.backward() and the Adam / torch_ema updates of
+ * model.py:99-106).  All f32, NHWC activations; csrc/train.hip. */
+
+/* dW[co][ky][kx][ci] += sum_p dY[p][co] X[p + (ky-1, kx-1)][ci] (ksize 3, pad 1) or the 1x1 form;
+ * X is the channel concatenation of x0 [.., C0] and x1 [.., C1]; dw must be zeroed by the caller. */
+int snrse_conv_wgrad(const float* dy, int Cout, const float* x0, int C0, const float* x1, int C1, int B, int H,
+                     int W, int ksize, float* dw, hipStream_t stream);
+/* scale * per-(b, c) sums over the HW pixels of x [B][HW][C] added into out_bc [B][C] and / or the
+ * per-c total into out_c [C] (bias, Dense_0 and temb gradients). */
+int snrse_chan_sum(const float* x, int B, int HW, int C, float* out_bc, float* out_c, float scale,
+                   hipStream_t stream);
+/* per-(b, group) mean and rstd = 1/sqrt(var + eps) from the slotted (sum, sumsq) statistics of the
+ * forward GroupNorm (snrse_gn_stats) of one or two channel-concatenated sources. */
+int snrse_gn_moments(const double* st0, int C0, const double* st1, int C1, int B, int HW, int groups, float eps,
+                     float* mean, float* rstd, hipStream_t stream);
+/* GroupNorm (+SiLU when act) backward (nn.GroupNorm layerspp.py:221,233; SiLU layers.py:38-39):
+ * dy [B][HW][C0+C1] -> dx0 [B][HW][C0], dx1 [B][HW][C1]; dgamma / dbeta [C] accumulated (+=);
+ * R: workspace of 2*B*(C0+C1) floats. */
+int snrse_gn_backward(const float* x0, int C0, const float* x1, int C1, const float* dy, int B, int HW,
+                      int groups, const float* gamma, const float* beta, const float* mean, const float* rstd,
+                      int act, float* R, float* dx0, float* dx1, float* dgamma, float* dbeta, hipStream_t stream);
+/* batched strided GEMM on MFMA: C[b](m,n) = alpha sum_k A[b](m,k) B[b](k,n) + beta C[b](m,n) (+ bias[n]),
+ * element (i, j) of operand X at X + b*sXb + i*sX(row) + j*sX(col); beta is 0 or 1. */
+int snrse_bgemm(const float* A, long long sAb, long long sAm, long long sAk, const float* Bm, long long sBb,
+                long long sBk, long long sBn, float* C, long long sCb, long long sCm, long long sCn, const float* bias,
+                int batch, int M, int N, int K, float alpha, float beta, hipStream_t stream);
+/* row softmax P = softmax(scale S) and its backward dS = scale P (dP - <dP, P>_row), rows of L. */
+int snrse_softmax_rows(const float* S, float* P, long long rows, int L, float scale, hipStream_t stream);
+int snrse_softmax_bwd_rows(const float* P, const float* dP, float* dS, long long rows, int L, float scale,
+                           hipStream_t stream);
+/* elementwise: y = silu(x); dx (+)= dy silu'(x); y = a x + b y; y = x * s[b] (recip: x / s[b]). */
+int snrse_silu(const float* x, float* y, long long n, hipStream_t stream);
+int snrse_silu_bwd(const float* x, const float* dy, float* dx, long long n, int accumulate, hipStream_t stream);
+int snrse_axpby(const float* x, float* y, long long n, float a, float b, hipStream_t stream);
+int snrse_scale_rows(const float* x, const float* s, float* y, int B, long long per, int recip, hipStream_t stream);
+/* GaussianFourierProjection of log t (layerspp.py:32-43): out [B][2 nf] = [sin, cos](2 pi log t W). */
+int snrse_gfp(const float* t, const float* Wg, int B, int nf, float* out, hipStream_t stream);
+/* perturbation of the consistency step on complex64 [B][HW]: mu = H(H^-1(x)(1 - w_b) + H^-1(y) w_b),
+ * x_t = mu + s_b z (H = exponent transform when transform != 0, model.py:304-312, 372-376). */
+int snrse_ct_perturb(const void* x, const void* y, const void* z, const float* wmix, const float* nscale, int B,
+                     int HW, int transform, void* mu, void* xt, hipStream_t stream);
+/* sebridge_v3 outputs f_k = cs_k x_k + co_k dnn_k (coef [B][4] = cs1, co1, cs0, co0), the mse
+ * (sqrt_loss = 0) or sqrt_mse (1) consistency loss per utterance into loss_b [B] (f64, the batch loss
+ * is their mean), and its gradient w.r.t. dnn1 / dnn0 (complex64 [B][HW], HW % 64 == 0). */
+int snrse_ct_loss(const void* dnn1, const void* dnn0, const void* x1, const void* x0, const float* coef, int B,
+                  int HW, int sqrt_loss, double* loss_b, void* g1, void* g0, hipStream_t stream);
+/* one torch.optim.Adam step (+ torch_ema update when a tensor's ema pointer is set) over a table of
+ * device tensors {float* p, const float* g, float* m, float* v, float* ema, int64 n} (device memory),
+ * split into chunks of 2048 elements (chunk_tensor / chunk_start, device arrays of nchunks). */
+int snrse_adam_ema(const void* tensors, const int* chunk_tensor, const long long* chunk_start, int nchunks,
+                   float lr, float beta1, float beta2, float eps, float bias_corr1, float bias_corr2_sqrt,
+                   float ema_decay, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

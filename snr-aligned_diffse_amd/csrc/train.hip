@@ -12,7 +12,7 @@
 //   snrse_softmax_rows    P = softmax(scale S) over rows; snrse_softmax_bwd_rows dS = P (dP - <dP, P>)
 //   snrse_silu_bwd        dx = dy silu'(x)
 //   snrse_axpby           y = a x + b y
-//   snrse_ct_perturb      mu_t = H(H^-1(x)(1-t) + H^-1(y) t), x_t = mu_t + t sigma_max z (model.py:372-376)
+//   snrse_ct_perturb      mu_t = H(H^-1(x)(1-w) + H^-1(y) w), x_t = mu_t + s z (model.py:304-312, 372-376)
 //   snrse_ct_loss         sebridge_v3 preconditioning of both evaluations + mse / sqrt_mse loss and its
 //                         gradient w.r.t. both network outputs (model.py:378-390, 536-541)
 //   snrse_adam_ema        torch.optim.Adam step (+ torch_ema 0.3 shadow update) over many tensors, one launch
@@ -358,17 +358,20 @@ SNRSE_DEV float2 spec_back1(float2 v) {
   return make_float2(v.x * mag, v.y * mag);
 }
 
-__global__ void ct_perturb_kernel(const float2* x, const float2* y, const float2* z, const float* t, int HW,
-                                  long long n, float sigma_max, int transform, float2* mu, float2* xt) {
+// mu = H(H^-1(x) (1 - w) + H^-1(y) w), x_t = mu + s z with per-utterance mixing weight w and noise scale s:
+// snr_conditioned 'true' w = t (model.py:372-376), 'fixed' w = fixed_snr t (x_ori + y0_ori fixed_snr t,
+// model.py:304-312); s = t sigma_max in both (z = randn * sigma_max)
+__global__ void ct_perturb_kernel(const float2* x, const float2* y, const float2* z, const float* wmix,
+                                  const float* nscale, int HW, long long n, int transform, float2* mu, float2* xt) {
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    const float tb = t[i / HW];
+    const float w = wmix[i / HW], sc = nscale[i / HW];
     float2 a = x[i], b = y[i];
     if (transform) { a = spec_back1(a); b = spec_back1(b); }
-    float2 m = make_float2(a.x * (1.f - tb) + b.x * tb, a.y * (1.f - tb) + b.y * tb);
+    float2 m = make_float2(a.x * (1.f - w) + b.x * w, a.y * (1.f - w) + b.y * w);
     if (transform) m = spec_fwd1(m);
     mu[i] = m;
     const float2 zz = z[i];
-    xt[i] = make_float2(m.x + tb * sigma_max * zz.x, m.y + tb * sigma_max * zz.y);
+    xt[i] = make_float2(m.x + sc * zz.x, m.y + sc * zz.y);
   }
 }
 
@@ -544,12 +547,12 @@ extern "C" int snrse_axpby(const float* x, float* y, long long n, float a, float
   return (int)hipGetLastError();
 }
 
-extern "C" int snrse_ct_perturb(const void* x, const void* y, const void* z, const float* t, int B, int HW,
-                                float sigma_max, int transform, void* mu, void* xt, hipStream_t s) {
-  if (!x || !y || !z || !t || !mu || !xt || B <= 0 || HW <= 0) return SNRSE_EINVAL;
+extern "C" int snrse_ct_perturb(const void* x, const void* y, const void* z, const float* wmix, const float* nscale,
+                                int B, int HW, int transform, void* mu, void* xt, hipStream_t s) {
+  if (!x || !y || !z || !wmix || !nscale || !mu || !xt || B <= 0 || HW <= 0) return SNRSE_EINVAL;
   const long long n = (long long)B * HW;
   hipLaunchKernelGGL(ct_perturb_kernel, dim3(grid_for(n)), dim3(256), 0, s, (const float2*)x, (const float2*)y,
-                     (const float2*)z, t, HW, n, sigma_max, transform, (float2*)mu, (float2*)xt);
+                     (const float2*)z, wmix, nscale, HW, n, transform, (float2*)mu, (float2*)xt);
   return (int)hipGetLastError();
 }
 

@@ -90,7 +90,8 @@ class NCSNpp(nn.Module):
         self.compute_dtype = compute_dtype
         self.output_layer = nn.Conv2d(4, 2, 1)
         mods = []
-        for m in _hip.build_plan(**self.cfg):
+        self._plan = _hip.build_plan(**self.cfg)
+        for m in self._plan:
             if m.kind == "gfp":
                 mods.append(GaussianFourierProjection(nf, fourier_scale))
             elif m.kind == "linear":

@@ -3,9 +3,10 @@
 Same constructor / attribute / method surface that eval.py and deep_eval.py use
 (load_from_checkpoint, eval(no_ema), sde, dnn, enhance, forward, get_pc_sampler, to_audio,
 _stft, _istft, _forward_transform, _backward_transform, t_eps, sigma_max, fixed_snr,
-model_type, snr_conditioned) on top of the HIP runtime.  Training (_step, validation,
-optimizer hooks) and the dead debug helpers (enhance_debug, prior_tests2, get_prior) are
-out of scope.
+model_type, snr_conditioned) on top of the HIP runtime, plus the consistency-training step of the paper's model
+(_step / training_step / configure_optimizers / optimizer_step for sebridge_v3 with
+snr_conditioned 'true' / 'fixed', SURVEY.md §8(f) 2, snrse/train.py).  Validation logging and
+the dead debug helpers (enhance_debug, prior_tests2, get_prior) are out of scope.
 
 Defined behaviour where the reference cannot run:
   * sebridge forward accepts t of shape [B] as well as [B,1,1,1] (the reference's
@@ -151,6 +152,50 @@ class ScoreModel(nn.Module):
             return xo, xm
 
         return step
+
+    # ------------------------------------------------------------------ training
+    def configure_optimizers(self):
+        """model.py:99-101: Adam(self.parameters(), lr) -- here the fused HIP Adam (snrse.train.FusedAdam)."""
+        from snrse.train import FusedAdam
+        return FusedAdam(self.parameters(), lr=self.lr)
+
+    def optimizer_step(self, optimizer, *args, **kwargs):
+        """model.py:103-106: the optimizer step, then the EMA update of the parameters; both run in the
+        single fused launch (the EMA shadows are updated with torch_ema's decay schedule)."""
+        optimizer.ema = self.ema
+        optimizer.step()
+
+    def _step(self, batch, batch_idx, valid=False, n=None, noise=None):
+        """Consistency-training loss of one batch (model.py:159-394) for model_type 'sebridge_v3' with
+        snr_conditioned 'true' (361-390) or 'fixed' (293-326), loss_type 'mse' / 'sqrt_mse'.
+        batch: (x, y) clean / noisy spectrograms [B, 1, F, T] (a Specs batch; valid=True takes
+        (x, y, s, n)).  n: grid indices [B] in 1..29 (default torch.randint(1, 30)); noise: the standard
+        complex normal draw of torch.randn_like(x) [B, 1, F, T] (default: in-kernel Philox).  Returns the
+        loss tensor; loss.backward() runs the HIP backward kernels and fills the parameters' .grad."""
+        from snrse import train as _train
+        if self.model_type != "sebridge_v3" or self.snr_conditioned not in ("true", "fixed"):
+            raise NotImplementedError("the HIP training step is built for model_type='sebridge_v3' with "
+                                      "snr_conditioned 'true' / 'fixed' (the paper's consistency training)")
+        self.data_module._check()
+        x, y = batch[0], batch[1]
+        B = x.shape[0]
+        dev = torch.device("cuda", torch.cuda.current_device())
+        X = x.to(dev, torch.complex64).reshape(B, x.shape[-2], x.shape[-1]).contiguous()
+        Y = y.to(dev, torch.complex64).reshape(B, y.shape[-2], y.shape[-1]).contiguous()
+        if n is None:
+            n = torch.randint(1, 30, (B,)).numpy()
+        n = np.asarray(n.cpu() if torch.is_tensor(n) else n).reshape(B)
+        if noise is None:
+            coef = torch.tensor([[0.0, 0.0, 0.0, 1.0]] * B, device=dev)
+            z = ops.axpby_noise(coef, like=X, seed=_noise_seed())
+        else:
+            z = noise.to(dev, torch.complex64).reshape(X.shape).contiguous()
+        return _train.consistency_loss(self.dnn, X, Y, n, z, float(self.sigma_max), self.loss_type,
+                                       fixed_snr=float(self.fixed_snr) if self.snr_conditioned == "fixed" else None,
+                                       transform=self.data_module.transform_type == "exponent")
+
+    def training_step(self, batch, batch_idx):
+        return self._step(batch, batch_idx, valid=False)
 
     # ------------------------------------------------------------------ samplers
     def get_pc_sampler(self, predictor_name, corrector_name, y, Y_prior=None, N=None, minibatch=None,

@@ -18,7 +18,7 @@ from .build import LIB
 
 F32, BF16, F16, F64 = 0, 1, 2, 3
 
-_vp, _i, _f, _u64 = C.c_void_p, C.c_int, C.c_float, C.c_uint64
+_vp, _i, _f, _u64, _ll = C.c_void_p, C.c_int, C.c_float, C.c_uint64, C.c_longlong
 
 # name -> argtypes (all return int status except the housekeeping ones)
 SIGNATURES = {
@@ -47,6 +47,22 @@ SIGNATURES = {
     "snrse_gn_resample": [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp],
     "snrse_gn_act": [_vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp],
     "snrse_set_workspace": [_vp, C.c_size_t],
+    # consistency-training step (csrc/train.hip)
+    "snrse_conv_wgrad": [_vp, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp],
+    "snrse_chan_sum": [_vp, _i, _i, _i, _vp, _vp, _f, _vp],
+    "snrse_gn_moments": [_vp, _i, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],
+    "snrse_gn_backward": [_vp, _i, _vp, _i, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "snrse_bgemm": [_vp, _ll, _ll, _ll, _vp, _ll, _ll, _ll, _vp, _ll, _ll, _ll, _vp, _i, _i, _i, _i, _f, _f, _vp],
+    "snrse_softmax_rows": [_vp, _vp, _ll, _i, _f, _vp],
+    "snrse_softmax_bwd_rows": [_vp, _vp, _vp, _ll, _i, _f, _vp],
+    "snrse_silu": [_vp, _vp, _ll, _vp],
+    "snrse_silu_bwd": [_vp, _vp, _vp, _ll, _i, _vp],
+    "snrse_axpby": [_vp, _vp, _ll, _f, _f, _vp],
+    "snrse_scale_rows": [_vp, _vp, _vp, _i, _ll, _i, _vp],
+    "snrse_gfp": [_vp, _vp, _i, _i, _vp, _vp],
+    "snrse_ct_perturb": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp],
+    "snrse_ct_loss": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp],
+    "snrse_adam_ema": [_vp, _vp, _vp, _i, _f, _f, _f, _f, _f, _f, _f, _vp],
 }
 HOUSEKEEPING = {"snrse_abi_version": ([], _i), "snrse_error_string": ([_i], C.c_char_p),
                 "snrse_device_name": ([C.c_char_p, _i], _i), "snrse_snrnet_workspace": ([_i, _i], C.c_size_t)}

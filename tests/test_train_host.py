@@ -1,0 +1,36 @@
+"""CPU checks of the consistency-training host logic (snrse/train.py): the t grid of model.py:366-367
+against the reference-generated golden, the sebridge_v3 preconditioning, and the drop-in API surface."""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+
+def test_t_grid_matches_reference_golden():
+    from snrse import train
+    g = golden("train_step.npz")
+    np.testing.assert_allclose(train.t_grid(g["n"]), g["t_n"], rtol=1e-6)
+    np.testing.assert_allclose(train.t_grid(g["n"] + 1), g["t_n1"], rtol=1e-6)
+    # the inference grid t_30 (model.py:22-23) is the same schedule over n = 1..30
+    from sgmse.model import t_30
+    np.testing.assert_allclose(train.t_grid(np.arange(1, 31)), t_30, rtol=1e-12)
+
+
+def test_precond_formula():
+    from snrse import train
+    t = np.array([0.001, 0.3, 1.0])
+    cs, co = train.precond(t)
+    np.testing.assert_allclose(cs, 0.25 / ((t - 0.001) ** 2 + 0.25))
+    np.testing.assert_allclose(co, 0.5 * (t - 0.001) / np.sqrt(0.25 + t ** 2))
+    assert co[0] == 0.0 and cs[0] == 1.0
+
+
+def test_training_api_surface_and_unsupported_branches():
+    import torch
+    from sgmse.model import ScoreModel
+    m = ScoreModel(backbone="ncsnpp", sde="ouve", model_type="bbed", theta=1.5, sigma_min=0.05, sigma_max=0.5)
+    for name in ("_step", "training_step", "configure_optimizers", "optimizer_step"):
+        assert callable(getattr(m, name))
+    x = torch.zeros(1, 1, 256, 64, dtype=torch.complex64)
+    with pytest.raises(NotImplementedError):
+        m._step((x, x), 0)

@@ -400,14 +400,80 @@ def gen_snr_enhance():
     save("enhance_snrnet_c4.npz", **{k: np.asarray(v) for k, v in out.items()})
 
 
+TRAIN_SHAPE = (2, 256, 64)  # B, F, T of the consistency-step golden (the reference trains on 256-frame crops)
+TRAIN_N = [3, 17]          # grid indices n (torch.randint(1, 30) in the reference)
+TRAIN_FULL = ["output_layer.weight", "output_layer.bias", "all_modules.1.bias", "all_modules.3.bias",
+              "all_modules.4.GroupNorm_0.weight", "all_modules.4.GroupNorm_0.bias", "all_modules.4.Conv_0.bias",
+              "all_modules.4.Dense_0.bias", "all_modules.7.Conv_0.weight", "all_modules.21.NIN_0.b",
+              "all_modules.21.GroupNorm_0.weight", "all_modules.33.NIN_3.b", "all_modules.75.weight",
+              "all_modules.76.weight", "all_modules.76.bias", "all_modules.74.Conv_2.bias"]
+TRAIN_HEAD = 96            # leading elements kept of every other gradient tensor
+
+
+def gen_train_step():
+    """the consistency-training loss of ScoreModel._step, sebridge_v3 +
+    snr_conditioned='true' (model.py:361-390, preconditioned forward 536-541), restated around the
+    REFERENCE NCSNpp module (formula weights) and differentiated by torch autograd on the CPU.  Both loss
+    types; the loss, every gradient's (sum, sum of squares, max |g|), the full gradient of a few tensors and
+    the first TRAIN_HEAD elements of every other one are stored."""
+    net = BackboneRegistry.get_by_name("ncsnpp")().train()
+    load_formula(net)
+    B, Fq, T = TRAIN_SHAPE
+    x = fnormal("golden.train.x", (B, 1, Fq, T), complex_=True) * 0.4
+    y = fnormal("golden.train.y", (B, 1, Fq, T), complex_=True) * 0.4 + x
+    z = fnormal("golden.train.z", (B, 1, Fq, T), complex_=True)
+    sigma_max, N, roh, eps, Tt = 0.5, 30, 7, 0.001, 1
+    n = torch.tensor(TRAIN_N).reshape(B, 1, 1, 1)
+    t_n = (eps ** (1 / roh) + ((n - 1) / (N - 1)) * (Tt ** (1 / roh) - eps ** (1 / roh))) ** roh
+    t_n1 = (eps ** (1 / roh) + ((n) / (N - 1)) * (Tt ** (1 / roh) - eps ** (1 / roh))) ** roh
+    zz = z * sigma_max
+    mu_t_n = spec_fwd_ref(spec_back_ref(x) * (1 - t_n) + spec_back_ref(y) * t_n)
+    mu_t_n1 = spec_fwd_ref(spec_back_ref(x) * (1 - t_n1) + spec_back_ref(y) * t_n1)
+    x_t_n = mu_t_n + t_n * zz
+    x_t_n1 = mu_t_n1 + t_n1 * zz
+
+    def forward(xx, t, yy):  # ScoreModel.forward, snr_conditioned 'true', sebridge_v3 (model.py:536-541)
+        e_, sd = 0.001, 0.5
+        c_skip = sd ** 2 / ((t - e_) ** 2 + sd ** 2)
+        c_out = (sd * (t - e_)) / ((sd ** 2 + t ** 2) ** 0.5)
+        return c_skip * xx + c_out * net(torch.cat([xx, yy], dim=1), t.squeeze(3).squeeze(2).squeeze(1))
+
+    out = {"n": np.asarray(TRAIN_N), "t_n": t2n(t_n).reshape(-1), "t_n1": t2n(t_n1).reshape(-1),
+           "full_keys": np.asarray(TRAIN_FULL), "head": np.int64(TRAIN_HEAD)}
+    names = [k for k, p in net.named_parameters() if p.requires_grad]
+    out["names"] = np.asarray(names)
+    for lt in ("mse", "sqrt_mse"):
+        net.zero_grad()
+        f_theta = forward(x_t_n1, t_n1, mu_t_n1)
+        f_theta_minus = forward(x_t_n, t_n, mu_t_n)
+        if lt == "mse":
+            err = f_theta - f_theta_minus
+        else:
+            sq = lambda f: f.abs() ** 0.5 * torch.exp(1j * f.angle())  # noqa: E731
+            err = sq(f_theta) - sq(f_theta_minus)
+        losses = torch.square(err.abs())
+        loss = torch.mean(0.5 * torch.sum(losses.reshape(losses.shape[0], -1), dim=-1))
+        loss.backward()
+        params = dict(net.named_parameters())
+        g = {k: params[k].grad.detach().double() for k in names}
+        out[f"{lt}_loss"] = np.float64(loss.item())
+        out[f"{lt}_gsum"] = np.asarray([float(g[k].sum()) for k in names])
+        out[f"{lt}_gsq"] = np.asarray([float((g[k] ** 2).sum()) for k in names])
+        out[f"{lt}_gmax"] = np.asarray([float(g[k].abs().max()) for k in names])
+        for k in TRAIN_FULL:
+            out[f"{lt}_full__{k}"] = t2n(g[k].float())
+        out[f"{lt}_head"] = np.concatenate([t2n(g[k].float()).reshape(-1)[:TRAIN_HEAD] for k in names])
+    save("train_step.npz", **out)
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["keys", "fir", "blocks", "attn", "ncsnpp", "sde", "pc_ouve",
-                             "pc_variants", "stft", "snrnet", "sebridge", "c4"]
+                             "pc_variants", "stft", "snrnet", "sebridge", "c4", "train"]
     table = {"keys": gen_keys, "fir": gen_fir, "blocks": gen_blocks, "attn": gen_attn,
              "ncsnpp": gen_ncsnpp, "sde": gen_sde, "pc_ouve": gen_pc_ouve,
              "pc_variants": gen_pc_variants, "stft": gen_stft, "snrnet": gen_snrnet,
-             "sebridge": gen_sebridge_enhance, "c4": gen_snr_enhance}
+             "sebridge": gen_sebridge_enhance, "c4": gen_snr_enhance, "train": gen_train_step}
     for w in which:
         torch.manual_seed(0)
         table[w]()
