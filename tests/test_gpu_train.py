@@ -6,10 +6,14 @@ with the REFERENCE NCSNpp module and torch autograd on the CPU (formula weights,
 n = (3, 17), formula noise).  Here the same batch runs through sgmse.model.ScoreModel._step on the
 HIP kernels (forward, backward and loss all HIP, snrse/train.py).
 
-Tolerances (fp32 on both sides, different summation orders): loss 1e-5 relative; gradients 1e-3
+Tolerances (fp32 on both sides, different summation orders): loss 3e-5 relative (a mean over
+2 x 256 x 64 complex bins whose value is ~2.5e4, summed in a different order); gradients 1e-3
 relative RMS over every tensor's stored elements and per-tensor sums of squares to 2e-3 (GroupNorm
 backward and the 3x3 wgrad reduce over up to 2 x 256 x 64 pixels in a different order than the
-CPU reference).
+CPU reference).  The attention KEY biases (NIN_1.b) are the exception: softmax over keys is
+invariant to adding q.b to every logit of a query, so their exact gradient is zero and both sides
+hold only rounding noise (~1e-7 of the query-bias gradient in the golden); for them the test checks
+that the HIP gradient is that small too, relative to the sibling query-bias (NIN_0.b) gradient.
 """
 import json
 import math
@@ -68,6 +72,12 @@ def test_consistency_step_loss_and_grads_vs_reference(gpu, loss_type):
     rel_head = float(np.sqrt(np.mean((got_head - ref_head) ** 2)) / np.sqrt(np.mean(ref_head ** 2)))
     ref_sq = g[f"{loss_type}_gsq"]
     rel_sq = np.abs(np.asarray(got_sq) - ref_sq) / np.maximum(ref_sq, 1e-30)
+    key_bias = {}
+    for i, k in enumerate(names):
+        if k.endswith("NIN_1.b"):
+            sib = names.index(k.replace("NIN_1.b", "NIN_0.b"))
+            key_bias[k] = math.sqrt(got_sq[i] / ref_sq[sib])
+            rel_sq[i] = 0.0
     full = {}
     for k in [str(s) for s in g["full_keys"]]:
         r = g[f"{loss_type}_full__{k}"].astype(np.float64)
@@ -79,8 +89,10 @@ def test_consistency_step_loss_and_grads_vs_reference(gpu, loss_type):
     with open(os.path.join(REPORT_DIR, f"train_step_{loss_type}_vs_reference.json"), "w") as f:
         json.dump({"loss": float(loss), "ref_loss": ref_loss, "rel_err_loss": err_loss,
                    "rel_rms_grad_heads": rel_head, "max_rel_err_grad_sumsq": float(rel_sq.max()),
-                   "worst_sumsq": worst, "rel_rms_full_tensors": full}, f, indent=1)
-    assert err_loss < 1e-5, err_loss
+                   "worst_sumsq": worst, "rel_rms_full_tensors": full,
+                   "key_bias_grad_norm_over_query_bias": key_bias}, f, indent=1)
+    assert err_loss < 3e-5, err_loss
+    assert len(key_bias) == 4 and max(key_bias.values()) < 1e-5, key_bias
     assert rel_head < 1e-3, (rel_head, worst)
     assert rel_sq.max() < 2e-3, worst
     assert max(full.values()) < 1e-3, full
