@@ -119,12 +119,13 @@ def _complex_noise(gen):
     return noise
 
 
-def cpu_baseline(seconds=4.0, n_steps=2, full=False):
+def cpu_baseline(seconds=4.0, n_steps=2, full=False, N=30):
     """The oracle (CPU restatement of the reference path, pinned to the reference goldens) on the
-    host: one synthetic 4 s clip, STFT + exponent transform -> prior -> `n_steps` PC steps with the
-    reference's reverse_diffusion + ALD algebra (sde_ref.pc_sample: 2 fp32 NCSN++ NFEs per step) ->
-    spec_back + iSTFT.  The per-NFE time (step algebra included) is extrapolated to N=30 (60 NFE).
-    full=True also runs the whole N=30 utterance once and reports it beside the extrapolation."""
+    host: one synthetic `seconds` clip, STFT + exponent transform -> prior -> `n_steps` PC steps with
+    the reference's reverse_diffusion + ALD algebra (sde_ref.pc_sample: 2 fp32 NCSN++ NFEs per step)
+    -> spec_back + iSTFT.  The per-NFE time (step algebra included) is extrapolated to N steps
+    (2N NFE).  full=True also runs the whole N=30 utterance once and reports it beside the
+    extrapolation."""
     from oracle import ncsnpp_ref, sde_ref, spec_ref
     env = _cpu_env()
     sd = ncsnpp_ref.state_dict_to_torch({k: v.numpy() for k, v in formula_weights().items()})
@@ -156,12 +157,12 @@ def cpu_baseline(seconds=4.0, n_steps=2, full=False):
         back(x, nf)
         t_back = time.perf_counter() - t0
         t_nfe = t_loop / nfe
-        t_utt = t_front + 60 * t_nfe + t_back
+        t_utt = t_front + 2 * N * t_nfe + t_back
         res = {"value": 1.0 / t_utt, "unit": "utt/s", "cores": env["cores"], "kind": "port",
                "sample": (f"1 synthetic {seconds:g} s clip through the oracle (CPU restatement, fp32): STFT + "
                           f"transform, {n_steps} reverse_diffusion+ALD PC steps ({nfe} NCSN++ NFEs at "
-                          f"[1,2,256,512] with the reference step algebra) + iSTFT; {t_nfe:.2f} s/NFE "
-                          f"extrapolated to N=30 (60 NFE/utt)"),
+                          f"[1,2,256,{Y.shape[-1]}] with the reference step algebra) + iSTFT; {t_nfe:.2f} s/NFE "
+                          f"extrapolated to N={N} ({2 * N} NFE/utt)"),
                "s_per_nfe": t_nfe, "cpu_model": env["cpu_model"], "os_cpu_count": env["os_cpu_count"]}
         if full:
             t0 = time.perf_counter()
@@ -403,6 +404,8 @@ def run(args):
         val = cpu_validation()
         if val is not None:
             cpu["validation"] = val
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c5":
+        cpu = cpu_baseline(seconds=args.seconds, n_steps=1, N=args.N)  # 2 NFEs of a 30 s clip
 
     n_frames = 1 + int(args.seconds * SR) // 128
     T_frames = (n_frames + 63) // 64 * 64

@@ -410,8 +410,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma_kernel(ConvParams p) {
   const int nbk = gridDim.x, bid = blockIdx.x;
   const int q8 = nbk >> 3, r8 = nbk & 7, xcd = bid & 7, pos = bid >> 3;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
-  const int m0 = (wg / p.ntn) * BM;
-  const int n0 = (wg % p.ntn) * BN;
+  // split-K (the small low-resolution levels of the fp32 path): the p.ksplit K ranges of one output
+  // tile are adjacent logical ids, i.e. on one XCD
+  const int ks = wg % p.ksplit, tl = wg / p.ksplit;
+  const int m0 = (tl / p.ntn) * BM;
+  const int n0 = (tl % p.ntn) * BN;
   const int HW = p.H * p.W;
   const int Cin = p.C0 + p.C1;
   const int cblocks = Cin / Tr::KT;
@@ -500,15 +503,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma_kernel(ConvParams p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  gload(0);
+  const int kb = (int)((long long)ks * nk / p.ksplit), ke = (int)((long long)(ks + 1) * nk / p.ksplit);
+  gload(kb);
   lstore(0);
   __syncthreads();
 
   const int lrow = lane & 15;
   const int lg = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
+  for (int kt = kb; kt < ke; ++kt) {
+    const int cur = (kt - kb) & 1;
+    if (kt + 1 < ke) gload(kt + 1);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       u32x4 af[FM], bfr[FN];
@@ -521,12 +525,26 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma_kernel(ConvParams p) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<T>(af[i], bfr[j], acc[i][j]);
     }
-    if (kt + 1 < nk) lstore(cur ^ 1);
+    if (kt + 1 < ke) lstore(cur ^ 1);
     __syncthreads();
   }
 
 #undef AS
 #undef BS
+  if (p.ksplit > 1) {  // raw fp32 partial sums of this K range; conv_splitk_finalize applies the epilogue
+    float* const wsp = p.ws + (size_t)ks * p.M * p.Cout;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm * TM + i * 16 + lg * 4 + e;
+        if (m < p.M) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) wsp[(size_t)m * p.Cout + n0 + wn * TN + j * 16 + lrow] = acc[i][j][e];
+        }
+      }
+    return;
+  }
   epilogue<TO, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, lane);
 }
 
@@ -1250,15 +1268,6 @@ int launch_halo5(ConvParams p, hipStream_t s) {
   return launch_halo5_gn<TO, 2>(p, s);
 }
 
-template <typename T, typename TO, int BM, int BN, int WM, int WN>
-int launch_conv(ConvParams p, int npad, hipStream_t s) {
-  p.ntn = npad / BN;
-  dim3 grid(((p.M + BM - 1) / BM) * p.ntn);
-  const size_t lds = (size_t)2 * (BM + BN) * 128;
-  hipLaunchKernelGGL((conv_mfma_kernel<T, TO, BM, BN, WM, WN>), grid, dim3(64 * WM * WN), lds, s, p);
-  return (int)hipGetLastError();
-}
-
 float* g_ws = nullptr;   // split-K workspace (snrse_set_workspace)
 size_t g_ws_bytes = 0;
 int g_splitk = 1;        // option "splitk": 0 disables K splitting
@@ -1269,13 +1278,36 @@ int g_last_ksplit = 1;   // option read-back "last_ksplit": splits of the latest
 // K splits for a v2 launch of `tiles` output tiles over nk K-tiles: about one workgroup per CU when
 // the tile grid alone underfills the chip (the small NCSN++ levels), >= 4 K-tiles per split, and
 // the partial sums within the registered workspace
-int choose_ksplit(const ConvParams& p, int tiles, int nk) {
+int choose_ksplit(const ConvParams& p, int tiles, int nk, int min_kt = 4) {
   if (!g_splitk || !g_ws || tiles >= g_splitk_target * 3 / 4) return 1;
   int s = (g_splitk_target + tiles - 1) / tiles;
-  if (s > nk / 4) s = nk / 4;
+  if (s > nk / min_kt) s = nk / min_kt;
   const size_t plane = (size_t)p.M * p.Cout * sizeof(float);
   if ((size_t)s * plane > g_ws_bytes) s = (int)(g_ws_bytes / plane);
   return s >= 2 ? s : 1;
+}
+
+// v1 register-staged GEMM (the fp32 parity path and the Cout <= 16 heads).  fp32 launches whose tile
+// grid underfills the chip (the low-resolution NCSN++ levels: 4-60 workgroups at 30 s, C5) split K
+// across workgroups (>= 2 K-tiles each) and finish in conv_splitk_finalize.
+template <typename T, typename TO, int BM, int BN, int WM, int WN>
+int launch_conv(ConvParams p, int npad, hipStream_t s) {
+  using Tr = ConvTraits<T>;
+  p.ntn = npad / BN;
+  const int tiles = ((p.M + BM - 1) / BM) * p.ntn;
+  const int nk = p.ksize * p.ksize * ((p.C0 + p.C1) / Tr::KT) + (p.sc_src ? (p.Csc + p.Csc1) / Tr::KT : 0);
+  p.ksplit = (sizeof(T) == 4 && BN == 128 && p.Cout % 128 == 0) ? choose_ksplit(p, tiles, nk, 2) : 1;
+  p.ws = g_ws;
+  g_last_ksplit = p.ksplit;
+  const size_t lds = (size_t)2 * (BM + BN) * 128;
+  hipLaunchKernelGGL((conv_mfma_kernel<T, TO, BM, BN, WM, WN>), dim3(tiles * p.ksplit), dim3(64 * WM * WN), lds, s, p);
+  if (p.ksplit > 1) {
+    SNRSE_LAUNCH_CHECK();
+    const int HW = p.H * p.W, ppb = 64;
+    hipLaunchKernelGGL((conv_splitk_finalize<TO>), dim3(p.B * ((HW + ppb - 1) / ppb), p.Cout / 128), dim3(256), 0, s,
+                       p, ppb);
+  }
+  return (int)hipGetLastError();
 }
 
 template <int BM, int BN, typename TO>
@@ -1303,12 +1335,13 @@ int launch_glds(ConvParams p, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 5 halo v5, 7 halo v7 (conv_halo7.hip; the
+// 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 5 halo v5, 7 halo v7 (conv_halo7.hip),
+// 9 halo v9 (conv_halo9.hip; bf16 output, Cin <= 512, else v5; the
 // experimental v3/v4/v6/v8 generations live in git history and tools/experimental/, outside the product
 // library)
 int g_conv_variant = 0;
 constexpr int kHaloAuto = 5;  // halo kernel generation taken by variant 0 (fastest measured: profiles/)
-int g_last_kernel = 0;        // option read-back "last_kernel": generation of the latest launch (9 = head)
+int g_last_kernel = 0;        // option read-back "last_kernel": generation of the latest launch (10 = head)
 
 template <typename T, typename TO>
 int dispatch_conv(const ConvParams& p, hipStream_t s) {
@@ -1321,12 +1354,12 @@ int dispatch_conv(const ConvParams& p, hipStream_t s) {
         if (g_conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0) {
           const int hk = g_conv_variant == 0 ? kHaloAuto : g_conv_variant;
           if constexpr (sizeof(TO) == 2) {
-            if (hk == 7 && halo7_ok(p)) {
+            if ((hk == 7 && halo7_ok(p)) || (hk == 9 && halo9_ok(p))) {
               ConvParams q = p;
               q.epi_nt = g_epi_nt == 2 ? ((long long)p.M * p.out_ld * 2 > (256ll << 20)) : g_epi_nt;
               g_last_epi_nt = q.epi_nt;
-              g_last_kernel = 7;
-              return launch_halo7(q, s);
+              g_last_kernel = hk;
+              return hk == 9 ? launch_halo9(q, s) : launch_halo7(q, s);
             }
           }
           g_last_kernel = 5;
@@ -1344,7 +1377,7 @@ int dispatch_conv(const ConvParams& p, hipStream_t s) {
   }
   if constexpr (sizeof(T) == 2 && sizeof(TO) == 4) {
     if (g_conv_variant != 1 && head_ok(p)) {
-      g_last_kernel = 9;
+      g_last_kernel = 10;
       return launch_head(p, s);
     }
   }
@@ -1464,7 +1497,7 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   if (!name || !value) return SNRSE_EINVAL;
   if (name_is(name, "conv_variant")) { *value = g_conv_variant; return 0; }
   if (name_is(name, "halo_kernel")) {  // generation taken by a halo-eligible bf16 conv
-    *value = g_conv_variant == 0 ? kHaloAuto : (g_conv_variant == 7 ? 7 : 5);
+    *value = g_conv_variant == 0 ? kHaloAuto : ((g_conv_variant == 7 || g_conv_variant == 9) ? g_conv_variant : 5);
     return 0;
   }
   if (name_is(name, "last_kernel")) { *value = g_last_kernel; return 0; }

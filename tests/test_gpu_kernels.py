@@ -33,13 +33,13 @@ def nchw(x):
 DT = {"f32": (torch.float32, 2e-6), "bf16": (torch.bfloat16, 1e-2)}
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 5, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 5, 7, 9])
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 16), (1, 256, 128, 4, 8), (3, 128, 256, 5, 7), (2, 384, 256, 4, 4),
                                    (2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (1, 256, 256, 12, 64)])
 def test_conv3x3(gpu, dt, shape, variant):
     """variant: 0 auto (the default halo GEMM where H%4==0, W%64==0), 1 register-staged, 2 LDS-DMA
-    im2col, 5 halo v5 forced, 7 halo v7 forced (bf16 output; f32 falls back to v5 / v1)."""
+    im2col, 5 halo v5 forced, 7 halo v7 forced, 9 halo v9 forced (bf16 output; f32 falls back to v5 / v1)."""
     from snrse import ops
     dtype, tol = DT[dt]
     B, cin, cout, H, W = shape
@@ -62,7 +62,7 @@ def test_conv3x3(gpu, dt, shape, variant):
 
 
 @pytest.mark.parametrize("epi_nt", [2, 0, 1])
-@pytest.mark.parametrize("variant", [0, 5, 7])
+@pytest.mark.parametrize("variant", [0, 5, 7, 9])
 @pytest.mark.parametrize("hw", [(8, 8), (8, 64)])
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 def test_conv_epilogue_shortcut_temb_comb(gpu, dt, hw, variant, epi_nt):
@@ -97,7 +97,7 @@ def test_conv_epilogue_shortcut_temb_comb(gpu, dt, hw, variant, epi_nt):
                          sc_wgt=w2.reshape(cout, cin).to(gpu, dtype).contiguous(), temb=temb.to(gpu), temb_off=20,
                          out_scale=1 / math.sqrt(2), comb=nhwc(pyr).to(gpu), comb_w=cw.to(gpu), comb_b=cb.to(gpu),
                          stats=st)
-        halo = ops.get_option("last_kernel") in (5, 7)
+        halo = ops.get_option("last_kernel") in (5, 7, 9)
         nt = ops.get_option("last_epi_nt")
     finally:
         ops.set_option("conv_variant", 0)
@@ -353,7 +353,7 @@ def test_philox_noise_statistics(gpu):
 
 
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (2, 256, 128, 4, 64)])
-@pytest.mark.parametrize("variant", [0, 5, 7])
+@pytest.mark.parametrize("variant", [0, 5, 7, 9])
 def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     """Halo GEMM consuming SiLU(GN(x)) from raw x + per-(b,c) scale/shift (+ raw 1x1 shortcut)."""
     from snrse import ops
@@ -391,7 +391,7 @@ def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     (8, 256, 0, 256, 64, 128, 0, 0, True, True, False, True),      # two Cout tiles per image
     (2, 256, 256, 256, 32, 64, 0, 0, False, False, True, False),   # cat input, no GN
 ])
-@pytest.mark.parametrize("variant", [5, 7])
+@pytest.mark.parametrize("variant", [5, 7, 9])
 def test_conv_halo_large(gpu, case, variant):
     """The halo GEMMs (v5, v7) vs an fp32 torch reference on the GPU at multi-image sizes, with
     the fused GroupNorm+SiLU prologue, cat inputs, the 1x1 shortcut, temb, residual and the
@@ -469,23 +469,28 @@ def test_gn_resample_tiled(gpu, mode, shape):
     assert rel(nchw(r.float()), ref_r) < 1e-2
 
 
-@pytest.mark.parametrize("out_f32", [False, True])
-def test_conv_splitk_small_levels(gpu, out_f32):
+@pytest.mark.parametrize("case", ["bf16", "bf16_f32out", "f32"])
+def test_conv_splitk_small_levels(gpu, case):
     """Small-image convs (the tile grid underfills the CUs) run as split-K GEMMs whose fp32 partial
     sums land in the registered workspace and are finished by conv_splitk_finalize (bias, temb,
-    residual, scale, GroupNorm statistics); they must agree with the unsplit GEMM and with fp64."""
+    residual, scale, GroupNorm statistics); they must agree with the unsplit GEMM and with fp64.
+    bf16: the LDS-DMA v2 GEMM; f32: the register-staged v1 GEMM of the fp32 parity path (C5)."""
     from snrse import ops
+    f32 = case == "f32"
+    out_f32 = case != "bf16"
     B, C0, C1, cout, H, W = 4, 256, 256, 256, 8, 16
-    x = torch.from_numpy(fnormal("t.sk.x", (B, C0 + C1, H, W))).bfloat16().float()
-    w = (torch.from_numpy(fnormal("t.sk.w", (cout, C0 + C1, 3, 3))) / 68).bfloat16().float()
+    idt = torch.float32 if f32 else torch.bfloat16
+    x = torch.from_numpy(fnormal("t.sk.x", (B, C0 + C1, H, W))).to(idt).float()
+    w = (torch.from_numpy(fnormal("t.sk.w", (cout, C0 + C1, 3, 3))) / 68).to(idt).float()
     b = torch.from_numpy(fnormal("t.sk.b", (cout,)))
     temb = torch.from_numpy(fnormal("t.sk.t", (B, 300)))
     odt = torch.float32 if out_f32 else torch.bfloat16
     r = torch.from_numpy(fnormal("t.sk.r", (B, cout, H, W))).to(odt).float()
     ref = (F.conv2d(x.double(), w.double(), b.double(), padding=1) + temb[:, 8:8 + cout, None, None].double()
            + r.double()) * 0.5
-    xg = nhwc(x).to(gpu, torch.bfloat16)
-    wp = w.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu, torch.bfloat16).contiguous()
+    tol, stol = (2e-6, 1e-5) if f32 else (1e-2, 3e-3)
+    xg = nhwc(x).to(gpu, idt)
+    wp = w.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu, idt).contiguous()
     outs = {}
     for sk in (0, 1):
         ops.set_option("splitk", sk)
@@ -499,11 +504,11 @@ def test_conv_splitk_small_levels(gpu, out_f32):
             ops.set_option("splitk", 1)
     assert outs[0][2] == 1 and outs[1][2] > 1
     for o, st, _ in outs.values():
-        assert rel(nchw(o.float()), ref) < 1e-2
+        assert rel(nchw(o.float()), ref) < tol
         od = o.double()
         st_ref = torch.stack([od.sum((1, 2)), (od * od).sum((1, 2))], -1)
-        assert rel(ops.fold_stats(st), st_ref) < 3e-3
-    assert rel(outs[1][0].float(), outs[0][0].float()) < 1e-2
+        assert rel(ops.fold_stats(st), st_ref) < stol
+    assert rel(outs[1][0].float(), outs[0][0].float()) < tol
 
 
 @pytest.mark.parametrize("shape", [(2, 128, 8, 64), (1, 256, 4, 128), (2, 128, 12, 64)])
