@@ -1335,10 +1335,9 @@ int launch_glds(ConvParams p, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 5 halo v5, 7 halo v7 (conv_halo7.hip),
-// 9 halo v9 (conv_halo9.hip; bf16 output, Cin <= 512, else v5; the
-// experimental v3/v4/v6/v8 generations live in git history and tools/experimental/, outside the product
-// library)
+// 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 5 halo v5; the experimental
+// v3/v4/v6/v7/v8/v9 generations (none faster than v5 on the NCSN++ shapes: profiles/r02d_h7_ablations.json,
+// profiles/r02g_conv_bench_v5_v7_v9.jsonl) live in git history and tools/experimental/, outside the product library
 int g_conv_variant = 0;
 constexpr int kHaloAuto = 5;  // halo kernel generation taken by variant 0 (fastest measured: profiles/)
 int g_last_kernel = 0;        // option read-back "last_kernel": generation of the latest launch (10 = head)
@@ -1352,17 +1351,7 @@ int dispatch_conv(const ConvParams& p, hipStream_t s) {
                         p.sc_bytes1 < 0x7ff00000ll;
       if (g_conv_variant != 1 && fits) {
         if (g_conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0) {
-          const int hk = g_conv_variant == 0 ? kHaloAuto : g_conv_variant;
-          if constexpr (sizeof(TO) == 2) {
-            if ((hk == 7 && halo7_ok(p)) || (hk == 9 && halo9_ok(p))) {
-              ConvParams q = p;
-              q.epi_nt = g_epi_nt == 2 ? ((long long)p.M * p.out_ld * 2 > (256ll << 20)) : g_epi_nt;
-              g_last_epi_nt = q.epi_nt;
-              g_last_kernel = hk;
-              return hk == 9 ? launch_halo9(q, s) : launch_halo7(q, s);
-            }
-          }
-          g_last_kernel = 5;
+          g_last_kernel = kHaloAuto;
           return launch_halo5<TO>(p, s);
         }
         if (p.gn_scale) return SNRSE_EINVAL;  // fused GroupNorm exists only on the halo paths
@@ -1497,7 +1486,7 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   if (!name || !value) return SNRSE_EINVAL;
   if (name_is(name, "conv_variant")) { *value = g_conv_variant; return 0; }
   if (name_is(name, "halo_kernel")) {  // generation taken by a halo-eligible bf16 conv
-    *value = g_conv_variant == 0 ? kHaloAuto : ((g_conv_variant == 7 || g_conv_variant == 9) ? g_conv_variant : 5);
+    *value = g_conv_variant == 0 ? kHaloAuto : 5;
     return 0;
   }
   if (name_is(name, "last_kernel")) { *value = g_last_kernel; return 0; }

@@ -92,13 +92,6 @@ SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, n, 0x00020000);
 }
 
-// v7 halo GEMM (conv_halo7.hip): bf16 3x3, H % 4 == 0, W % 64 == 0, Cout % 128 == 0, bf16 output.
-int launch_halo7(const ConvParams& p, hipStream_t s);
-bool halo7_ok(const ConvParams& p);
-// v9 halo GEMM (conv_halo9.hip): v7's tile with a double-buffered halo transformed between the MFMA
-// bursts; additionally Cin <= 512.
-int launch_halo9(const ConvParams& p, hipStream_t s);
-bool halo9_ok(const ConvParams& p);
 // Pyramid heads (conv_head.hip): 3x3, Cout <= 16, f32 output, optional fused GroupNorm+SiLU.
 int launch_head(const ConvParams& p, hipStream_t s);
 bool head_ok(const ConvParams& p);

@@ -95,8 +95,7 @@ def get_option(name):
     return v.value
 
 
-KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 5: "conv_halo5_kernel", 7: "conv_halo7_kernel", 9: "conv_halo9_kernel",
-           10: "conv_head_kernel"}
+KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 5: "conv_halo5_kernel", 10: "conv_head_kernel"}
 
 
 def kernel_name(gen):
@@ -114,7 +113,7 @@ def halo_ok(x, ksize, cout):
     qualifies: sources beyond 2 GiB run as consecutive launches over image ranges (snrse_conv2d)."""
     B, H, W, C = x.shape
     return (x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and H % 4 == 0 and W % 64 == 0
-            and _VARIANT["v"] in (0, 5, 7, 9))
+            and _VARIANT["v"] in (0, 5))
 
 
 def head_ok(x):

@@ -33,7 +33,7 @@ def nchw(x):
 DT = {"f32": (torch.float32, 2e-6), "bf16": (torch.bfloat16, 1e-2)}
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 5, 7, 9])
+@pytest.mark.parametrize("variant", [0, 1, 2, 5])
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 16), (1, 256, 128, 4, 8), (3, 128, 256, 5, 7), (2, 384, 256, 4, 4),
                                    (2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (1, 256, 256, 12, 64)])
@@ -62,7 +62,7 @@ def test_conv3x3(gpu, dt, shape, variant):
 
 
 @pytest.mark.parametrize("epi_nt", [2, 0, 1])
-@pytest.mark.parametrize("variant", [0, 5, 7, 9])
+@pytest.mark.parametrize("variant", [0, 5])
 @pytest.mark.parametrize("hw", [(8, 8), (8, 64)])
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 def test_conv_epilogue_shortcut_temb_comb(gpu, dt, hw, variant, epi_nt):
@@ -97,7 +97,7 @@ def test_conv_epilogue_shortcut_temb_comb(gpu, dt, hw, variant, epi_nt):
                          sc_wgt=w2.reshape(cout, cin).to(gpu, dtype).contiguous(), temb=temb.to(gpu), temb_off=20,
                          out_scale=1 / math.sqrt(2), comb=nhwc(pyr).to(gpu), comb_w=cw.to(gpu), comb_b=cb.to(gpu),
                          stats=st)
-        halo = ops.get_option("last_kernel") in (5, 7, 9)
+        halo = ops.get_option("last_kernel") == 5
         nt = ops.get_option("last_epi_nt")
     finally:
         ops.set_option("conv_variant", 0)
@@ -353,7 +353,7 @@ def test_philox_noise_statistics(gpu):
 
 
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (2, 256, 128, 4, 64)])
-@pytest.mark.parametrize("variant", [0, 5, 7, 9])
+@pytest.mark.parametrize("variant", [0, 5])
 def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     """Halo GEMM consuming SiLU(GN(x)) from raw x + per-(b,c) scale/shift (+ raw 1x1 shortcut)."""
     from snrse import ops
@@ -391,7 +391,7 @@ def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     (8, 256, 0, 256, 64, 128, 0, 0, True, True, False, True),      # two Cout tiles per image
     (2, 256, 256, 256, 32, 64, 0, 0, False, False, True, False),   # cat input, no GN
 ])
-@pytest.mark.parametrize("variant", [5, 7, 9])
+@pytest.mark.parametrize("variant", [5])
 def test_conv_halo_large(gpu, case, variant):
     """The halo GEMMs (v5, v7) vs an fp32 torch reference on the GPU at multi-image sizes, with
     the fused GroupNorm+SiLU prologue, cat inputs, the 1x1 shortcut, temb, residual and the
