@@ -1476,6 +1476,8 @@ extern "C" int snrse_debug_set_stamps(void* buf) {
 }
 #endif
 
+extern __attribute__((visibility("hidden"))) int g_resample_variant, g_resample_nt;  // resample.hip
+
 static bool name_is(const char* a, const char* b) {
   int i = 0;
   while (a[i] && a[i] == b[i]) ++i;
@@ -1498,6 +1500,8 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   if (name_is(name, "last_ksplit")) { *value = g_last_ksplit; return 0; }
   if (name_is(name, "last_epi_nt")) { *value = g_last_epi_nt; return 0; }
   if (name_is(name, "last_chunks")) { *value = g_last_chunks; return 0; }
+  if (name_is(name, "resample_variant")) { *value = g_resample_variant; return 0; }
+  if (name_is(name, "resample_nt")) { *value = g_resample_nt; return 0; }
   return SNRSE_EINVAL;
 }
 
@@ -1510,6 +1514,8 @@ extern "C" int snrse_set_option(const char* name, int value) {
   if (name_is(name, "epi_nt")) { g_epi_nt = value; return 0; }
   if (name_is(name, "h5_stagger")) { g_h5_stagger_per_phase = value; return 0; }
   if (name_is(name, "stats_zeroed")) { g_snrse_stats_zeroed = value ? 1 : 0; return 0; }
+  if (name_is(name, "resample_variant")) { g_resample_variant = value; return 0; }
+  if (name_is(name, "resample_nt")) { g_resample_nt = value; return 0; }
   return SNRSE_EINVAL;
 }
 

@@ -15,6 +15,11 @@
 
 #include <type_traits>
 
+// option "resample_variant" (snrse_set_option): 0 auto (row strips where C / 8 divides 64), 1 tiled
+__attribute__((visibility("hidden"))) int g_resample_variant = 0;
+// option "resample_nt": 1 = non-temporal stores in the row-strip kernel
+__attribute__((visibility("hidden"))) int g_resample_nt = 0;
+
 namespace {
 
 constexpr int kCB = 16;  // channels per block (two 8 x bf16 vectors per pixel)
@@ -225,9 +230,251 @@ __global__ __launch_bounds__(256) void gn_act_kernel(const bf16_t* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Row-strip variant (default where C / 8 divides 64).  The tiled kernel above gives each block 16
+// channels of a pixel tile, so every wave-wide load or store touches 32 B of each 256-B pixel (C = 128)
+// and the lines are completed by other blocks; at level 0 that ran at ~3 TB/s.  Here a thread owns one
+// 8-channel vector of ONE output row over a segment of L output positions, and the NV = C / 8 lanes of a
+// pixel are adjacent, so each wave instruction moves 64 / NV whole pixels (full 128-B lines).  The
+// separable FIR [1,3,3,1] runs in registers: the vertical taps per input column (act and raw), then the
+// horizontal taps over a sliding window of column values.  The GroupNorm + SiLU of an input vector is
+// recomputed by each output row that reads it (2x down, 4x up; VALU, not bytes).
+//   down: out(oy, ox) = sum_ab k[a] k[b] x(2oy-1+a, 2ox-1+b), k = [1,3,3,1]/8
+//   up:   out(2p+i, 2q+j) from input rows {p-1, p} (i = 0) or {p, p+1} (i = 1) with weights (1/4, 3/4) /
+//         (3/4, 1/4), and the same in columns: out(.., 2q) = (V(q-1) + 3 V(q)) / 4, out(.., 2q+1) =
+//         (3 V(q) + V(q+1)) / 4
+// Zero padding applies to the activated tensor and to x (out-of-image vectors are 0 for both).
+
+template <int CPT> struct RVec;  // CPT channels of one pixel: 16 B (8 ch) or 8 B (4 ch)
+template <> struct RVec<8> {
+  typedef u32x4 T;
+  SNRSE_DEV static T load(__amdgpu_buffer_rsrc_t r, int off) { return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0); }
+  SNRSE_DEV static void unpack(const T v, float* x) { unpack8(v, x); }
+  SNRSE_DEV static T pack(const float* x) { return pack8(x); }
+};
+template <> struct RVec<4> {
+  typedef __attribute__((ext_vector_type(2))) unsigned int T;
+  SNRSE_DEV static T load(__amdgpu_buffer_rsrc_t r, int off) { return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0); }
+  SNRSE_DEV static void unpack(const T v, float* x) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      x[2 * i] = __uint_as_float(v[i] << 16);
+      x[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+    }
+  }
+  SNRSE_DEV static T pack(const float* x) { return T{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])}; }
+};
+
+template <int CPT> struct RowVec {  // act and raw values of one CPT-channel vector
+  float a[CPT], r[CPT];
+};
+
+SNRSE_DEV __amdgpu_buffer_rsrc_t rs_rsrc(const void* base, unsigned bytes) {
+  const uint64_t a = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// Strips are numbered per image up to a multiple of the strips of one wave (64 / NV), so a wave never
+// straddles two images: the image base is wave-uniform (one buffer resource, 32-bit offsets, hardware
+// zero-fill of out-of-image vectors).  NV lanes (CPT channels each) cover one pixel, C = NV * CPT.
+template <int MODE, int NV, int CPT>
+__global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __restrict__ src, int H, int W, int L,
+                                                               int nseg, int nrows, const float* __restrict__ scale,
+                                                               const float* __restrict__ shift, int act,
+                                                               bf16_t* __restrict__ out_act,
+                                                               bf16_t* __restrict__ out_raw, int nblk, int B,
+                                                               int sp_img, int nt) {
+  using V = RVec<CPT>;
+  constexpr int C = NV * CPT, SPB = 256 / NV;  // strips per block
+  // XCD-aware bijective remap: consecutive logical blocks (neighbouring output rows, which share input
+  // rows) run on one XCD and its L2
+  const int q8 = nblk >> 3, r8 = nblk & 7, xcd = blockIdx.x & 7, pos = blockIdx.x >> 3;
+  const int lb = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
+  const int v = threadIdx.x % NV;
+  const int gs = lb * SPB + threadIdx.x / NV;
+  const int b = __builtin_amdgcn_readfirstlane(gs / sp_img);
+  const int ls = gs - b * sp_img;  // strip within the image
+  if (b >= B || ls >= nrows * nseg) return;  // padding strips
+  const int seg = ls % nseg;
+  const int orow = ls / nseg;  // output row
+  const int Ho = MODE == MODE_DOWN ? H / 2 : 2 * H, Wo = MODE == MODE_DOWN ? W / 2 : 2 * W;
+  float sc[CPT], sh[CPT];
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    sc[i] = scale ? scale[(size_t)b * C + CPT * v + i] : 1.f;
+    sh[i] = scale ? shift[(size_t)b * C + CPT * v + i] : 0.f;
+  }
+  const __amdgpu_buffer_rsrc_t rsrc = rs_rsrc(src + (size_t)b * H * W * C, (unsigned)((size_t)H * W * C * 2));
+  constexpr int NR = MODE == MODE_DOWN ? 4 : 2;  // input rows per output row
+  int iy0;
+  float wy[NR];
+  if constexpr (MODE == MODE_DOWN) {
+    iy0 = 2 * orow - 1;
+    wy[0] = 0.125f; wy[1] = 0.375f; wy[2] = 0.375f; wy[3] = 0.125f;
+  } else {
+    const int p = orow >> 1;
+    iy0 = (orow & 1) ? p : p - 1;
+    wy[0] = (orow & 1) ? 0.75f : 0.25f;
+    wy[1] = 1.f - wy[0];
+  }
+  bool rowok[NR];
+#pragma unroll
+  for (int a = 0; a < NR; ++a) rowok[a] = iy0 + a >= 0 && iy0 + a < H;
+
+  // vertical taps of input column ix -> column value (act, raw); the loads are issued one step ahead of
+  // their use (software pipelining: the next column's vectors are in flight while this one is filtered)
+  struct Raw {
+    typename V::T x[NR];
+  };
+  auto load_col = [&](int ix) {
+    Raw rw;
+    const bool colok = ix >= 0 && ix < W;
+#pragma unroll
+    for (int a = 0; a < NR; ++a) {
+      const bool ok = colok && rowok[a];
+      rw.x[a] = V::load(rsrc, ok ? (((iy0 + a) * W + ix) * C + CPT * v) * 2 : (int)0x80000000);  // outside: 0
+    }
+    return rw;
+  };
+  auto eval_col = [&](const Raw& rw, int ix) {
+    const bool colok = ix >= 0 && ix < W;
+    RowVec<CPT> cv;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) { cv.a[i] = 0.f; cv.r[i] = 0.f; }
+#pragma unroll
+    for (int a = 0; a < NR; ++a) {
+      float x[CPT];
+      V::unpack(rw.x[a], x);
+      const bool ok = colok && rowok[a];
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const float y = fmaf(x[i], sc[i], sh[i]);
+        const float t = ok ? (act ? silu(y) : y) : 0.f;
+        cv.a[i] = fmaf(t, wy[a], cv.a[i]);
+        cv.r[i] = fmaf(x[i], wy[a], cv.r[i]);
+      }
+    }
+    return cv;
+  };
+  auto column = [&](int ix) { return eval_col(load_col(ix), ix); };
+  auto store = [&](int ox, const float* a, const float* r) {
+    const size_t o = (((size_t)b * Ho + orow) * Wo + ox) * C + CPT * v;
+    if (nt) {
+      __builtin_nontemporal_store(V::pack(a), (typename V::T*)(out_act + o));
+      if (out_raw) __builtin_nontemporal_store(V::pack(r), (typename V::T*)(out_raw + o));
+    } else {
+      *(typename V::T*)(out_act + o) = V::pack(a);
+      if (out_raw) *(typename V::T*)(out_raw + o) = V::pack(r);
+    }
+  };
+
+  if constexpr (MODE == MODE_DOWN) {
+    // out(ox) = k0 V(2ox-1) + k1 V(2ox) + k1 V(2ox+1) + k0 V(2ox+2): carry only the partial sum of the
+    // two columns shared with the previous output
+    const int ox0 = seg * L, ox1 = min(Wo, ox0 + L);
+    float pa[CPT], pr[CPT];
+    {
+      const RowVec<CPT> c0 = column(2 * ox0 - 1), c1 = column(2 * ox0);
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        pa[i] = 0.125f * c0.a[i] + 0.375f * c1.a[i];
+        pr[i] = 0.125f * c0.r[i] + 0.375f * c1.r[i];
+      }
+    }
+    Raw n2 = load_col(2 * ox0 + 1), n3 = load_col(2 * ox0 + 2);
+    for (int ox = ox0; ox < ox1; ++ox) {
+      const Raw r2 = n2, r3 = n3;
+      if (ox + 1 < ox1) {
+        n2 = load_col(2 * ox + 3);
+        n3 = load_col(2 * ox + 4);
+      }
+      const RowVec<CPT> c2 = eval_col(r2, 2 * ox + 1), c3 = eval_col(r3, 2 * ox + 2);
+      float oa[CPT], orw[CPT];
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        oa[i] = fmaf(0.125f, c3.a[i], fmaf(0.375f, c2.a[i], pa[i]));
+        orw[i] = fmaf(0.125f, c3.r[i], fmaf(0.375f, c2.r[i], pr[i]));
+        pa[i] = fmaf(0.375f, c3.a[i], 0.125f * c2.a[i]);
+        pr[i] = fmaf(0.375f, c3.r[i], 0.125f * c2.r[i]);
+      }
+      store(ox, oa, orw);
+    }
+  } else {
+    // output columns 2q, 2q+1 for input columns q in [q0, q1)
+    const int q0 = seg * L, q1 = min(W, q0 + L);
+    RowVec<CPT> cm = column(q0 - 1), cc = column(q0);
+    Raw np = load_col(q0 + 1);
+    for (int q = q0; q < q1; ++q) {
+      const Raw rp = np;
+      if (q + 1 < q1) np = load_col(q + 2);
+      const RowVec<CPT> cp = eval_col(rp, q + 1);
+      float ea[CPT], er[CPT], oa[CPT], orw[CPT];
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        ea[i] = 0.25f * cm.a[i] + 0.75f * cc.a[i];
+        er[i] = 0.25f * cm.r[i] + 0.75f * cc.r[i];
+        oa[i] = 0.75f * cc.a[i] + 0.25f * cp.a[i];
+        orw[i] = 0.75f * cc.r[i] + 0.25f * cp.r[i];
+      }
+      store(2 * q, ea, er);
+      store(2 * q + 1, oa, orw);
+      cm = cc;
+      cc = cp;
+    }
+  }
+}
+
+template <int MODE, int NV, int CPT>
+int launch_rows(const void* src, int B, int H, int W, const float* scale, const float* shift, int act, void* out_act,
+                void* out_raw, hipStream_t stream) {
+  const int nrows = MODE == MODE_DOWN ? H / 2 : 2 * H;
+  const int span = MODE == MODE_DOWN ? W / 2 : W;  // positions a strip walks (output cols / input cols)
+  // strip length: 16 positions, shortened on small images until the grid has >= 2^17 threads (8 waves
+  // per CU)
+  int L = span >= 16 ? 16 : span;
+  while (L > 1 && (long long)B * nrows * ((span + L - 1) / L) * NV < (1 << 17)) L >>= 1;
+  const int nseg = (span + L - 1) / L;
+  constexpr int SPB = 256 / NV, SPW = 64 / NV;
+  const long long sp_img = ((long long)nrows * nseg + SPW - 1) / SPW * SPW;  // strips per image, padded
+  const long long nblk = (sp_img * B + SPB - 1) / SPB;
+  if (nblk > 0x7fffffffLL || sp_img * B > 0x7fffffffLL || (long long)H * W * NV * CPT * 2 >= 0x7fffffffLL)
+    return SNRSE_EINVAL;
+  hipLaunchKernelGGL((gn_resample_rows_kernel<MODE, NV, CPT>), dim3((unsigned)nblk), dim3(256), 0, stream,
+                     (const bf16_t*)src, H, W, L, nseg, nrows, scale, shift, act, (bf16_t*)out_act, (bf16_t*)out_raw,
+                     (int)nblk, B, (int)sp_img, g_resample_nt);
+  return (int)hipGetLastError();
+}
+
+// down: 4 channels per lane (8 input vectors per output column pair stay within 4 waves per SIMD);
+// up: 8 channels per lane (16-B stores)
+template <int MODE>
+int dispatch_rows(const void* src, int C, int B, int H, int W, const float* scale, const float* shift, int act,
+                  void* out_act, void* out_raw, hipStream_t stream) {
+  constexpr int CPT = MODE == MODE_DOWN ? 4 : 8;
+  if (C % CPT) return -1;
+  switch (C / CPT) {
+    case 1: return launch_rows<MODE, 1, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 2: return launch_rows<MODE, 2, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 4: return launch_rows<MODE, 4, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 8: return launch_rows<MODE, 8, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 16: return launch_rows<MODE, 16, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 32: return launch_rows<MODE, 32, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 64: return launch_rows<MODE, 64, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    default: return -1;  // not handled here
+  }
+}
+
 template <int MODE>
 int launch_resample(const void* src, int C, int B, int H, int W, const float* scale, const float* shift, int act,
                     void* out_act, void* out_raw, hipStream_t stream) {
+  if (g_resample_variant == 0) {
+    const int r = dispatch_rows<MODE>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    if (r >= 0) return r;
+  }
+  if (C % kCB) return SNRSE_EINVAL;
   using T = RTile<MODE>;
   const int Ho = MODE == MODE_DOWN ? H / 2 : 2 * H, Wo = MODE == MODE_DOWN ? W / 2 : 2 * W;
   const int tiles_y = (Ho + T::OTY - 1) / T::OTY, tiles_x = (Wo + T::OTX - 1) / T::OTX;
@@ -243,7 +490,7 @@ int launch_resample(const void* src, int C, int B, int H, int W, const float* sc
 extern "C" int snrse_gn_resample(const void* src, int C, int B, int H, int W, const float* scale,
                                  const float* shift, int act, int mode, void* out_act, void* out_raw,
                                  hipStream_t stream) {
-  if (!src || !out_act || C <= 0 || C % kCB || B <= 0 || H <= 0 || W <= 0 || (!scale) != (!shift))
+  if (!src || !out_act || C <= 0 || C % 8 || B <= 0 || H <= 0 || W <= 0 || (!scale) != (!shift))
     return SNRSE_EINVAL;
   if (mode == MODE_DOWN) {
     if ((H & 1) || (W & 1)) return SNRSE_EINVAL;

@@ -258,7 +258,7 @@ def gn_apply(src0, src1=None, sums=None, gamma=None, beta=None, act=True, mode="
 def gn_resample(x, scale=None, shift=None, act=True, mode="down", want_raw=False):
     """act(x*scale+shift) FIR-resampled x2 ('down' / 'up': upfirdn2d with [1,3,3,1]) and, with
     want_raw, the FIR of x itself (the ResBlock shortcut input) from one LDS-tiled pass over x
-    (snrse_gn_resample; bf16, C % 16 == 0).  Returns (activated, raw or None)."""
+    (snrse_gn_resample; bf16, C % 8 == 0 with C / 8 dividing 64, or C % 16 == 0).  Returns (activated, raw or None)."""
     _dev(x, scale, shift)
     if x.dtype != torch.bfloat16:
         raise TypeError("snrse: gn_resample takes bf16 activations")

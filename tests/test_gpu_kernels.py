@@ -445,14 +445,19 @@ def test_conv_halo_large(gpu, case, variant):
         assert rel(ops.fold_stats(st), st_ref) < 3e-3
 
 
+@pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("mode", ["down", "up"])
-@pytest.mark.parametrize("shape", [(2, 128, 8, 16), (1, 256, 36, 70), (3, 16, 18, 34), (1, 32, 9, 21)])
-def test_gn_resample_tiled(gpu, mode, shape):
-    """LDS-tiled GroupNorm+SiLU+FIR and, in the same pass, the raw FIR of the shortcut input
-    (layerspp.py:245-257), with partial tiles at the image edges, against the oracle FIR applied to
-    an fp64 GroupNorm+SiLU."""
+@pytest.mark.parametrize("shape", [(2, 128, 8, 16), (1, 256, 36, 70), (3, 16, 18, 34), (1, 32, 9, 21),
+                                   (2, 128, 64, 256), (1, 512, 6, 40), (2, 8, 8, 8)])
+def test_gn_resample_tiled(gpu, mode, shape, variant):
+    """GroupNorm+SiLU+FIR and, in the same pass, the raw FIR of the shortcut input
+    (layerspp.py:245-257), with partial tiles / strips at the image edges, against the oracle FIR
+    applied to an fp64 GroupNorm+SiLU.  variant 0: the row-strip kernel (C / 8 dividing 64), 1: the
+    LDS-tiled kernel (C % 16 == 0)."""
     from snrse import ops
     B, C, H, W = shape
+    if variant == 1 and C % 16:
+        pytest.skip("the tiled kernel takes C % 16 == 0")
     if mode == "down" and (H % 2 or W % 2):
         pytest.skip("down-sampling needs even H and W")
     x = (torch.from_numpy(fnormal("t.rs.x", (B, C, H, W))) * 2 + 0.3).bfloat16().float()
@@ -464,7 +469,11 @@ def test_gn_resample_tiled(gpu, mode, shape):
     xg = nhwc(x).to(gpu, torch.bfloat16)
     sums, _ = ops.gn_stats(xg)
     scale, shift = ops.gn_scale_shift(sums, g.to(gpu), be.to(gpu), H * W)
-    a, r = ops.gn_resample(xg, scale, shift, act=True, mode=mode, want_raw=True)
+    ops.set_option("resample_variant", variant)
+    try:
+        a, r = ops.gn_resample(xg, scale, shift, act=True, mode=mode, want_raw=True)
+    finally:
+        ops.set_option("resample_variant", 0)
     assert rel(nchw(a.float()), ref_a) < 1e-2
     assert rel(nchw(r.float()), ref_r) < 1e-2
 
