@@ -141,3 +141,64 @@ def test_spawn_ranks_world2(tmp_path):
     assert sd.spawn_ranks(2, _spawned_child, (path,)) == 0
     assert open(path).read() == "2 1.0 [0.0, 0.0, 0.0, 1.0, 1.0, 1.0]"
     assert sd.spawn_ranks(2, _failing_child) == 3
+
+
+def _deep_eval_worker(rank, world, port, root, out, q):
+    """deep_evaluate() (the deep_eval.py SNR sweep) on gloo with a stand-in model: each rank enhances
+    the nine SNR variants of its files, the rows meet in one all_gather, rank 0 writes the tables."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from snrse import deep_evaluate as de
+    from snrse import dist as sd
+    r, w, _ = sd.init_from_env("gloo")
+
+    class _SDE:
+        _T = 1.0
+
+    class _Model:
+        sde = _SDE()
+        seen = []
+
+        def enhance(self, x, y, **kw):
+            self.seen.append(kw["noise_rms"])
+            return (0.5 * y[0]).numpy()
+
+    m = _Model()
+    data = de.deep_evaluate(m, root, out, N=30, rank=r, world=w, batched=False, verbose=False)
+    q.put((r, len(m.seen), data["filename"], data["pesq_-5"], sorted(set(round(v, 6) for v in m.seen))))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_gloo_world2_deep_evaluate_sharded(tmp_path):
+    import numpy as np
+
+    from snrse import audio
+    root = tmp_path / "t"
+    for d in ("clean", "noisy"):
+        os.makedirs(root / d)
+    for k in range(3):
+        sig = np.full(800 + 10 * k, 0.25, np.float32)
+        audio.write_wav(str(root / "clean" / f"u{k}.wav"), sig, bits=32)
+        audio.write_wav(str(root / "noisy" / f"u{k}.wav"), sig * 1.5, bits=32)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    out = str(tmp_path / "out")
+    procs = [ctx.Process(target=_deep_eval_worker, args=(r, 2, port, str(root), out, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, n0, f0, p0, rms0), (r1, n1, f1, p1, rms1) = res
+    assert (n0, n1) == (2 * 9, 1 * 9)                # contiguous shards, nine variants per file
+    assert f0 == f1 == ["u0.wav", "u1.wav", "u2.wav"] and len(p0) == 3
+    assert rms0 == sorted(round(10 ** ((5 - s) / 20), 6) for s in range(0, 41, 5))  # deep_eval.py:118
+    lines = open(os.path.join(out, "_results_deep.csv")).read().splitlines()
+    assert lines[0] == "filename," + ",".join(f"pesq_{s - 5}" for s in range(0, 41, 5)) and len(lines) == 4
+    for s in range(0, 41, 5):
+        assert os.path.exists(os.path.join(out, "{0:02d}".format(s - 5), "u2.wav"))
+    txt = open(os.path.join(out, "_avg_results_deep.txt")).read().splitlines()
+    assert txt[0].startswith("PESQ_-5: ") and txt[-1].startswith("PESQ_35: ") and len(txt) == 9

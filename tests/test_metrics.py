@@ -121,3 +121,20 @@ def test_evaluate_driver_end_to_end(tmp_path):
         ref = np_energy_ratios(outs[k], x[0].numpy(), (y - x)[0].numpy())
         np.testing.assert_allclose([data["si_sdr"][k], data["si_sir"][k], data["si_sar"][k]], ref, atol=1e-5)
     assert (out / "_results.csv").exists() and (out / "_avg_results.txt").exists()
+
+
+def test_deep_eval_snr_variants_match_reference_arithmetic():
+    """deep_eval.py:108-118 in torch float32 (the reference's tensors) vs snr_variants."""
+    from snrse import deep_evaluate as de
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal(999).astype(np.float32) * 0.1
+    y = (x + rng.standard_normal(999).astype(np.float32) * 0.05).astype(np.float32)
+    ys, noise_rms = de.snr_variants(x, y)
+    xt, yt = torch.from_numpy(x)[None], torch.from_numpy(y)[None]
+    y0 = yt - xt
+    for k, S in enumerate(range(0, 41, 5)):
+        ref = (xt + y0 * 10 ** (-S / 20)).numpy()[0]
+        np.testing.assert_array_equal(ys[k], ref)
+        assert noise_rms[k] == 10 ** ((-S + 5) / 20)
+    assert de.LABELS == (-5, 0, 5, 10, 15, 20, 25, 30, 35)
+    assert ["{0:02d}".format(v) for v in de.LABELS][:3] == ["-5", "00", "05"]
