@@ -197,9 +197,22 @@ SNRSE_DEV float sum_lanes_strided(float v) {
 // Lean LDS-staged epilogue of the halo kernels: the wave's 64 rows are 64 consecutive pixels of
 // image `b` and its 64 channels are in range (H % 4 == 0, W % 64 == 0, Cout % 128 == 0 there), so
 // bias / temb / Combine weights are per-lane constants and no row or column masking is needed.
-template <typename TO, int NWM, int BN, bool DEFER>
+// Epilogue flags as a compile-time mask (EF >= 0: the v5 halo GEMM's common configurations, no
+// per-pass branches) or read from the parameters at run time (EF = -1).
+enum { EF_TEMB = 1, EF_RES = 2, EF_COMB = 4, EF_STATS = 8, EF_NT = 16, EF_RT = -1 };
+inline int epi_flags(const ConvParams& p) {  // host side (launch dispatch)
+  return (p.temb ? EF_TEMB : 0) | (p.res ? EF_RES : 0) | (p.comb_src ? EF_COMB : 0) | (p.stats ? EF_STATS : 0) |
+         (p.epi_nt ? EF_NT : 0);
+}
+
+template <typename TO, int NWM, int BN, bool DEFER, int EF = EF_RT>
 SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int mb, int nb, int lane, float* stage,
                             float* red, int wm, int b, int blk_n0) {
+  const bool f_temb = EF < 0 ? p.temb != nullptr : (EF & EF_TEMB) != 0;
+  const bool f_res = EF < 0 ? p.res != nullptr : (EF & EF_RES) != 0;
+  const bool f_comb = EF < 0 ? p.comb_src != nullptr : (EF & EF_COMB) != 0;
+  const bool f_stats = EF < 0 ? p.stats != nullptr : (EF & EF_STATS) != 0;
+  const bool f_nt = EF < 0 ? p.epi_nt != 0 : (EF & EF_NT) != 0;
   constexpr int LDR = 68;
   constexpr int EPC = 16 / (int)sizeof(TO);
   constexpr int NCH = 64 / EPC;
@@ -223,13 +236,13 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
       add[k] += v[0]; add[k + 1] += v[1]; add[k + 2] += v[2]; add[k + 3] += v[3];
     }
   }
-  if (p.temb) {
+  if (f_temb) {
     const float* tb = p.temb + (size_t)b * p.temb_stride + n;
 #pragma unroll
     for (int k = 0; k < EPC; ++k) add[k] += tb[k];
   }
   float cw[EPC][4], cb[EPC];
-  if (p.comb_src) {
+  if (f_comb) {
 #pragma unroll
     for (int k = 0; k < EPC; ++k) {
       const f32x4 w = *(const f32x4*)(p.comb_w + (size_t)(n + k) * 4);
@@ -250,12 +263,12 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
   u32x4 rpre[PRE ? NPASS : 1];
   f32x4 qpre[PRE ? NPASS : 1];
   if constexpr (PRE) {
-    if (p.res) {
+    if (f_res) {
 #pragma unroll
       for (int pass = 0; pass < NPASS; ++pass)
         rpre[pass] = *(const u32x4*)((const TO*)p.res + ((size_t)mb + r0 + pass * RPP) * p.res_ld + n);
     }
-    if (p.comb_src) {
+    if (f_comb) {
 #pragma unroll
       for (int pass = 0; pass < NPASS; ++pass) qpre[pass] = *(const f32x4*)(p.comb_src + ((size_t)mb + r0 + pass * RPP) * 4);
     }
@@ -270,7 +283,7 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
     const float* sr = stage + row * LDR + cc * EPC;
 #pragma unroll
     for (int k = 0; k < EPC; ++k) v[k] = sr[k] + add[k];
-    if (p.res) {
+    if (f_res) {
       u32x4 rv;
       if constexpr (PRE) rv = rpre[pass];
       else rv = *(const u32x4*)((const TO*)p.res + m * p.res_ld + n);
@@ -287,7 +300,7 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
     }
 #pragma unroll
     for (int k = 0; k < EPC; ++k) v[k] *= p.out_scale;
-    if (p.comb_src) {
+    if (f_comb) {
       f32x4 q;
       if constexpr (PRE) q = qpre[pass];
       else q = *(const f32x4*)(p.comb_src + m * 4);
@@ -302,16 +315,16 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] = __float_as_uint(v[k]);
     }
-    if (p.epi_nt)  // option "epi_nt": streaming (non-temporal) output stores
+    if (f_nt)  // option "epi_nt": streaming (non-temporal) output stores
       __builtin_nontemporal_store(o, (u32x4*)((TO*)p.out + m * p.out_ld + n));
     else
       *(u32x4*)((TO*)p.out + m * p.out_ld + n) = o;
-    if (p.stats) {
+    if (f_stats) {
 #pragma unroll
       for (int k = 0; k < EPC; ++k) { s1[k] += v[k]; s2[k] = fmaf(v[k], v[k], s2[k]); }
     }
   }
-  if (p.stats) {
+  if (f_stats) {
 #pragma unroll
     for (int k = 0; k < EPC; ++k) {
       s1[k] = sum_lanes_strided<NCH>(s1[k]);
@@ -964,7 +977,7 @@ SNRSE_DEV uint32_t gn_xform2(uint32_t v, float s0, float h0, float s1, float h1)
   return pack_bf16x2(lo, hi);
 }
 
-template <typename TO, int GNM>
+template <typename TO, int GNM, int EF>
 __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   constexpr bool H5SW = SNRSE_H5_SWAP && sizeof(TO) == 2;  // swapped operands + register epilogue
   constexpr int TH = 4, TW = 64, HC = TW + 2;
@@ -1189,14 +1202,14 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   if constexpr (H5SW) {
     epilogue_swapped<TO>(p, acc, mrow, n0, lane, red, wid, bb);
   } else {
-    epilogue_img<TO, 4, 128, true>(p, acc[0], mrow, n0, lane, stage, red, wid, bb, n0);
+    epilogue_img<TO, 4, 128, true, EF>(p, acc[0], mrow, n0, lane, stage, red, wid, bb, n0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     SNRSE_STAMP(26);
-    epilogue_img<TO, 4, 128, true>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0);
+    epilogue_img<TO, 4, 128, true, EF>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0);
   }
   SNRSE_STAMP(27);
-  if (p.stats) block_stats_flush<4, 128>(p, red, bb, n0);
+  if (EF < 0 ? p.stats != nullptr : (EF & EF_STATS) != 0) block_stats_flush<4, 128>(p, red, bb, n0);
   }  // tile loop
 #ifdef SNRSE_STAMPS
   {
@@ -1228,6 +1241,20 @@ int g_h5_persist = 0;                 // option "h5_persist": persistent stagger
                                       // 5-10 % slower than one tile per workgroup: off)
 int g_h5_slots = 512;                 // two workgroups per CU (256 CUs)
 int g_h5_stagger_per_phase = 3600;    // option "h5_stagger": s_memtime ticks per phase x nq / 2
+int g_h5_specialise = 1;              // option "h5_specialise": compile-time epilogue flags for the common
+                                      // bf16 configurations (0: the run-time flags everywhere)
+
+template <typename TO, int GNM, int EF>
+int launch_halo5_ef(ConvParams p, int grid, size_t lds, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    SNRSE_RET(hipFuncSetAttribute((const void*)conv_halo5_kernel<TO, GNM, EF>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv_halo5_kernel<TO, GNM, EF>), dim3(grid), dim3(256), lds, s, p);
+  return (int)hipGetLastError();
+}
 
 template <typename TO, int GNM>
 int launch_halo5_gn(ConvParams p, hipStream_t s) {
@@ -1236,12 +1263,6 @@ int launch_halo5_gn(ConvParams p, hipStream_t s) {
 #else
   constexpr size_t lds = 396 * 64 + 2 * 3 * 128 * 64;
 #endif
-  static bool attr = false;
-  if (!attr) {
-    SNRSE_RET(hipFuncSetAttribute((const void*)conv_halo5_kernel<TO, GNM>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
-  }
   p.ntn = p.Cout / 128;
   p.epi_nt = g_epi_nt == 2 ? ((long long)p.M * p.out_ld * (long long)sizeof(TO) > (256ll << 20)) : g_epi_nt;
   g_last_epi_nt = p.epi_nt;
@@ -1256,8 +1277,27 @@ int launch_halo5_gn(ConvParams p, hipStream_t s) {
     const int nq = 3 * ((p.C0 + p.C1) / 32) + (p.sc_src ? (p.Csc + p.Csc1) / 32 : 0);
     p.h5_stagger = g_h5_stagger_per_phase * nq / 2;
   }
-  hipLaunchKernelGGL((conv_halo5_kernel<TO, GNM>), dim3(grid), dim3(256), lds, s, p);
-  return (int)hipGetLastError();
+  // the bf16 ResBlock configurations of the NCSN++ path get a branch-free epilogue (bias always on):
+  // Conv_0 (+temb), Conv_1 (+residual | +1x1 shortcut as extra K | +Combine), each +-stats, +-NT
+  if constexpr (sizeof(TO) == 2 && GNM != 1) {
+    if (g_h5_specialise && p.bias) {
+      switch (epi_flags(p)) {
+#define SNRSE_H5_EF(F) \
+  case (F): return launch_halo5_ef<TO, GNM, (F)>(p, grid, lds, s);
+        SNRSE_H5_EF(EF_TEMB | EF_STATS)
+        SNRSE_H5_EF(EF_TEMB | EF_STATS | EF_NT)
+        SNRSE_H5_EF(EF_RES | EF_STATS)
+        SNRSE_H5_EF(EF_RES | EF_STATS | EF_NT)
+        SNRSE_H5_EF(EF_STATS)
+        SNRSE_H5_EF(EF_STATS | EF_NT)
+        SNRSE_H5_EF(EF_COMB | EF_STATS)
+        SNRSE_H5_EF(EF_TEMB)
+#undef SNRSE_H5_EF
+        default: break;
+      }
+    }
+  }
+  return launch_halo5_ef<TO, GNM, EF_RT>(p, grid, lds, s);
 }
 
 // GroupNorm prologue mode as a template argument: the halo transform is straight-line code
@@ -1496,6 +1536,7 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   if (name_is(name, "h5_persist")) { *value = g_h5_persist; return 0; }
   if (name_is(name, "epi_nt")) { *value = g_epi_nt; return 0; }
   if (name_is(name, "h5_stagger")) { *value = g_h5_stagger_per_phase; return 0; }
+  if (name_is(name, "h5_specialise")) { *value = g_h5_specialise; return 0; }
   if (name_is(name, "stats_zeroed")) { *value = g_snrse_stats_zeroed; return 0; }
   if (name_is(name, "last_ksplit")) { *value = g_last_ksplit; return 0; }
   if (name_is(name, "last_epi_nt")) { *value = g_last_epi_nt; return 0; }
@@ -1513,6 +1554,7 @@ extern "C" int snrse_set_option(const char* name, int value) {
   if (name_is(name, "h5_persist")) { g_h5_persist = value; return 0; }
   if (name_is(name, "epi_nt")) { g_epi_nt = value; return 0; }
   if (name_is(name, "h5_stagger")) { g_h5_stagger_per_phase = value; return 0; }
+  if (name_is(name, "h5_specialise")) { g_h5_specialise = value; return 0; }
   if (name_is(name, "stats_zeroed")) { g_snrse_stats_zeroed = value ? 1 : 0; return 0; }
   if (name_is(name, "resample_variant")) { g_resample_variant = value; return 0; }
   if (name_is(name, "resample_nt")) { g_resample_nt = value; return 0; }

@@ -89,6 +89,10 @@ def load(path: str | None = None) -> C.CDLL:
         fn.argtypes = args
         fn.restype = res
     _lib = lib
+    # SNRSE_OPTS="name=value,..." sets library options at load time (A/B runs of bench.py / tools)
+    for kv in filter(None, os.environ.get("SNRSE_OPTS", "").split(",")):
+        k, v = kv.split("=")
+        check(lib.snrse_set_option(k.strip().encode(), int(v)), f"snrse_set_option({k})")
     return lib
 
 

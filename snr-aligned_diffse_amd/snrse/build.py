@@ -18,6 +18,12 @@ LIB = os.path.join(LIBDIR, "libsnrse_hip.so")
 ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wno-unused-result"]
+# Files whose kernels interleave VALU work with MFMAs: no SLP vectorisation, which otherwise packs
+# adjacent f32 adds / muls / fmas into v_pk_*_f32 -- slower than the scalar forms beside MFMAs
+# (MI355X_MICROARCH.md, 'price of one filler beside MFMAs'; measured +1.8 % C2 utt/s, halo GEMM
+# 703 -> 686 us per launch, profiles/r02n_noslp_ab.json)
+FILE_FLAGS = {name: ["-fno-slp-vectorize"] for name in ("conv.hip", "conv_head.hip", "attn.hip", "score.hip",
+                                                          "train.hip")}
 
 
 def _sources():
@@ -32,11 +38,11 @@ def needs_build() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(f) > t for f in _sources() + _headers())
+    return any(os.path.getmtime(f) > t for f in _sources() + _headers() + [os.path.abspath(__file__)])
 
 
 def _compile(src: str, obj: str, extra=()):
-    cmd = [HIPCC, *FLAGS, *extra, "-c", src, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *extra, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
@@ -50,7 +56,7 @@ def build_library(force: bool = False, jobs: int = 8, extra_flags=(), lib: str =
         return LIB
     objdir = os.path.join(os.path.dirname(lib), "obj")
     os.makedirs(objdir, exist_ok=True)
-    hdr_t = max([os.path.getmtime(h) for h in _headers()] + [0.0])
+    hdr_t = max([os.path.getmtime(h) for h in _headers() + [os.path.abspath(__file__)]] + [0.0])
     todo, objs = [], []
     for src in _sources():
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
