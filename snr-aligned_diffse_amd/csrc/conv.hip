@@ -964,17 +964,37 @@ SNRSE_DEV void epilogue_swapped(const ConvParams& p, const f32x4 (&acc)[2][4][4]
   }
 }
 
-// GroupNorm prologue of the v5 halo kernel on one packed bf16 pair: GNM 1 = affine, 2 = affine + SiLU
+// GroupNorm prologue of the v5 halo kernel on one 16-B vector (8 bf16 channels): GNM 1 = affine,
+// 2 = affine + SiLU; `ok` = inside the image (else the conv's zero padding).  Written stage by stage
+// over the 8 elements (8 independent exp / rcp chains) so the schedule can hide the transcendental
+// latencies; element by element the chain was fully serial with an s_nop after every exp and rcp.
 template <int GNM>
-SNRSE_DEV uint32_t gn_xform2(uint32_t v, float s0, float h0, float s1, float h1) {
-  float lo = __uint_as_float(v << 16), hi = __uint_as_float(v & 0xffff0000u);
-  lo = fmaf(lo, s0, h0);
-  hi = fmaf(hi, s1, h1);
-  if constexpr (GNM == 2) {
-    lo = silu(lo);
-    hi = silu(hi);
+SNRSE_DEV u32x4 gn_xform8(const u32x4 v, const float* sc, const float* sh, bool ok) {
+  float y[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    y[2 * i] = fmaf(__uint_as_float(v[i] << 16), sc[2 * i], sh[2 * i]);
+    y[2 * i + 1] = fmaf(__uint_as_float(v[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]);
   }
-  return pack_bf16x2(lo, hi);
+  if constexpr (GNM == 2) {
+    // sched_barrier(0) between the stages: without it the scheduler (at the kernel's 256-VGPR limit)
+    // re-serialises the 8 chains to save registers
+    float e[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_exp2f(y[k] * -1.44269504088896341f);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_rcpf(1.0f + e[k]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) y[k] *= e[k];
+  }
+  // zero padding as an AND mask: a select here becomes an exec-masked branch around the whole transform
+  const uint32_t okm = 0u - (uint32_t)ok;
+  u32x4 o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = pack_bf16x2(y[2 * i], y[2 * i + 1]) & okm;
+  return o;
 }
 
 template <typename TO, int GNM, int EF>
@@ -1099,13 +1119,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
       if (j == HJ - 1 && hr >= HROWS) break;
       u32x4 v = hv[j];
       if constexpr (GNM > 0) {
-        if (tr) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t o = gn_xform2<GNM>(v[i], gsc[2 * i], gsh[2 * i], gsc[2 * i + 1], gsh[2 * i + 1]);
-            v[i] = hok[j] ? o : 0u;  // outside the image: the conv's zero padding
-          }
-        }
+        if (tr) v = gn_xform8<GNM>(v, gsc, gsh, hok[j]);  // outside the image: the conv's zero padding
       }
       *(u32x4*)(halo + swz64(hr, hcol)) = v;
     }
