@@ -193,37 +193,64 @@ def c1_clip():
     return (np.concatenate(list(g["noisy_i16"]))[: 4 * SR].astype(np.float32) / 32768.0)[None]
 
 
+def oracle_one_step(y, sd, ssd, noise, fixed_snr=0.17783, sigma_max=0.5):
+    """The reference's SNR-aligned one-step enhance (model.py:713-833, sebridge_v3 + snr_conditioned
+    'true') through the oracle on the CPU: y [1, L] numpy -> (x_hat [L], t_hat)."""
+    from oracle import ncsnpp_ref, snrnet_ref, spec_ref
+    nf0 = float(np.abs(y).max())
+    raw = spec_ref.stft(y / nf0)
+    T16 = raw.shape[-1] + (16 - raw.shape[-1] % 16) % 16
+    R = np.zeros((1, 256, T16), np.complex64)
+    R[..., : raw.shape[-1]] = raw
+    Rt = torch.from_numpy(R)
+    g = snrnet_ref.snrnet_forward(torch.stack([Rt.real, Rt.imag], 1), ssd)
+    est = float(g[0, 0] / (1 - g[0, 0]))
+    t_hat = snrnet_ref.snap_t(est, fixed_snr)
+    norm = nf0 * snrnet_ref.normfac(t_hat, fixed_snr)
+    Y = torch.from_numpy(spec_ref.pad_spec(spec_ref.spec_fwd(spec_ref.stft(y / norm))).astype(np.complex64))[:, None]
+    X = Y + noise(Y.shape) * sigma_max * t_hat
+    tt = torch.tensor([t_hat], dtype=torch.float32)
+    c_skip = 0.25 / ((t_hat - 0.001) ** 2 + 0.25)
+    c_out = 0.5 * (t_hat - 0.001) / math.sqrt(0.25 + t_hat ** 2)
+    s = c_skip * X + c_out * ncsnpp_ref.ncsnpp_forward(torch.cat([X, Y], 1), tt, sd)
+    return spec_ref.istft(spec_ref.spec_back(s[0, 0].numpy()), y.shape[1]) * norm, t_hat
+
+
+def cpu_baseline_c4(seconds=4.0, n=3):
+    """C4's CPU leg: `n` synthetic clips through the oracle's one-step SNR-aligned enhance (SNRNet
+    estimate + one fp32 NCSN++ evaluation + STFT / iSTFT), after one warm-up clip."""
+    from oracle import ncsnpp_ref
+    env = _cpu_env()
+    sd = ncsnpp_ref.state_dict_to_torch({k: v.numpy() for k, v in formula_weights().items()})
+    ssd = {k: v.float() for k, v in snrnet_formula_sd().items()}
+    ys = synth_clips(n + 1, seconds, 20_000)
+    noise = _complex_noise(torch.Generator().manual_seed(2))
+    with torch.no_grad():
+        oracle_one_step(ys[:1], sd, ssd, noise)
+        t0 = time.perf_counter()
+        for k in range(1, n + 1):
+            oracle_one_step(ys[k:k + 1], sd, ssd, noise)
+        el = time.perf_counter() - t0
+    return {"value": n / el, "unit": "utt/s", "cores": env["cores"], "kind": "port",
+            "sample": (f"{n} synthetic {seconds:g} s clips through the oracle (CPU restatement, fp32): SNRNet "
+                       f"estimate + t_hat snap + one preconditioned NCSN++ NFE + STFT / iSTFT each"),
+            "cpu_model": env["cpu_model"], "os_cpu_count": env["os_cpu_count"]}
+
+
 def run_c1(args):
     """configs[0]: the reference's CPU-runnable case, --gpus 0.  One 4 s VBD utterance, sebridge_v3,
     exponent transform, SNR from SNRNet, on PyTorch CPU via the oracle: the one-step enhance
     (model.py:713-833; N is ignored on this branch) timed `--steps` times, plus one N=5 PC run
     (10 NFE, model.py:756-768 arithmetic) as the plumbing check of the sampler path."""
-    from oracle import ncsnpp_ref, sde_ref, snrnet_ref, spec_ref
+    from oracle import ncsnpp_ref, sde_ref, spec_ref
     env = _cpu_env()
     sd = ncsnpp_ref.state_dict_to_torch({k: v.numpy() for k, v in formula_weights().items()})
     ssd = {k: v.float() for k, v in snrnet_formula_sd().items()}
     y = c1_clip()
-    fixed_snr, sigma_max = 0.17783, 0.5
     noise = _complex_noise(torch.Generator().manual_seed(1))
 
     def one_step():
-        nf0 = float(np.abs(y).max())
-        raw = spec_ref.stft(y / nf0)
-        T16 = raw.shape[-1] + (16 - raw.shape[-1] % 16) % 16
-        R = np.zeros((1, 256, T16), np.complex64)
-        R[..., : raw.shape[-1]] = raw
-        Rt = torch.from_numpy(R)
-        g = snrnet_ref.snrnet_forward(torch.stack([Rt.real, Rt.imag], 1), ssd)
-        est = float(g[0, 0] / (1 - g[0, 0]))
-        t_hat = snrnet_ref.snap_t(est, fixed_snr)
-        norm = nf0 * snrnet_ref.normfac(t_hat, fixed_snr)
-        Y = torch.from_numpy(spec_ref.pad_spec(spec_ref.spec_fwd(spec_ref.stft(y / norm))).astype(np.complex64))[:, None]
-        X = Y + noise(Y.shape) * sigma_max * t_hat
-        tt = torch.tensor([t_hat], dtype=torch.float32)
-        c_skip = 0.25 / ((t_hat - 0.001) ** 2 + 0.25)
-        c_out = 0.5 * (t_hat - 0.001) / math.sqrt(0.25 + t_hat ** 2)
-        s = c_skip * X + c_out * ncsnpp_ref.ncsnpp_forward(torch.cat([X, Y], 1), tt, sd)
-        return spec_ref.istft(spec_ref.spec_back(s[0, 0].numpy()), y.shape[1]) * norm, t_hat
+        return oracle_one_step(y, sd, ssd, noise)
 
     with torch.no_grad():
         for _ in range(args.warmup):
@@ -406,6 +433,8 @@ def run(args):
             cpu["validation"] = val
     elif rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c5":
         cpu = cpu_baseline(seconds=args.seconds, n_steps=1, N=args.N)  # 2 NFEs of a 30 s clip
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c4":
+        cpu = cpu_baseline_c4(seconds=args.seconds)
 
     n_frames = 1 + int(args.seconds * SR) // 128
     T_frames = (n_frames + 63) // 64 * 64
