@@ -87,6 +87,23 @@ def test_snrnet_golden(gpu):
     np.testing.assert_allclose(y.cpu().numpy(), g["out"], rtol=2e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("B,T", [(3, 80), (2, 512)])
+def test_snrnet_vs_oracle_larger(gpu, B, T):
+    """The tiled SNRNet kernels (conv stages staged in LDS, weights broadcast) against the oracle's
+    restatement of snrnet.py:47-97 on CPU, at the C4 frame count (T=512) and with a partial last
+    block of 16 chunks (B=3, T=80: 15 chunks)."""
+    from oracle import snrnet_ref
+    from sgmse.backbones import SNRNet
+    sd = {k: torch.from_numpy(v) for k, v in formula_sd("snrnet", "snrnet.").items()}
+    net = SNRNet()
+    net.load_state_dict(sd)
+    net = net.cuda()
+    x = torch.from_numpy(fnormal(f"t.snrnet.{B}.{T}", (B, 2, 256, T)))
+    y = net(x.to(gpu)).cpu()
+    ref = snrnet_ref.snrnet_forward(x, {k: v.float() for k, v in sd.items()})
+    np.testing.assert_allclose(y.numpy(), ref.numpy(), rtol=1e-4, atol=1e-6)
+
+
 def test_data_module_golden(gpu):
     from sgmse.data_module import SpecsDataModule
     g = golden("stft.npz")
