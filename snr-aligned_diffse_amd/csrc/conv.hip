@@ -1447,7 +1447,7 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
   if (C0 % KT || C1 % KT || (sc_src && (Csc % KT || Csc1 % KT))) return SNRSE_EINVAL;
   if (sc_src && Csc1 > 0 && !sc_src1) return SNRSE_EINVAL;
   if (C1 > 0 && !src1) return SNRSE_EINVAL;
-  ConvParams p;
+  ConvParams p{};
   p.src0 = src0; p.C0 = C0; p.src1 = src1; p.C1 = C1;
   p.B = B; p.H = H; p.W = W; p.ksize = ksize; p.wgt = wgt;
   p.sc_src = sc_src; p.Csc = sc_src ? Csc : 0; p.sc_wgt = sc_wgt;
