@@ -347,10 +347,72 @@ def pmc_traffic(kernel_prefix, tag):
     return None, None
 
 
+# ----------------------------------------------------------------------------- training step
+def run_train(args):
+    """consistency-training steps of the SNR-aligned sebridge_v3 model (model.py:361-390,
+    loss mse) on the HIP forward + backward kernels, fused Adam + EMA (model.py:99-106): synthetic
+    complex spectrogram pairs [B, 1, 256, T] (the data module's training crop, num_frames 256), fp32 as
+    the reference trains.  One step = training_step -> loss.backward() -> optimizer_step -> zero_grad."""
+    from sgmse.model import ScoreModel
+    from snrse import ops
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    hp = dict(backbone="ncsnpp", sde="ouve", model_type="sebridge_v3", snr_conditioned="true", theta=1.5,
+              sigma_min=0.05, sigma_max=0.5, N=30, compute_dtype="fp32", fixed_snr=0.17783, loss_type="mse")
+    m = ScoreModel(**hp)
+    m.dnn.load_state_dict(formula_weights())
+    m = m.cuda().train()
+    opt = m.configure_optimizers()
+    B, T = args.batch, args.frames
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = (torch.randn(B, 1, 256, T, dtype=torch.complex64, device=dev, generator=g) * 0.4)
+    y = x + torch.randn(B, 1, 256, T, dtype=torch.complex64, device=dev, generator=g) * 0.4
+
+    def step(i):
+        loss = m.training_step((x, y), i)
+        loss.backward()
+        m.optimizer_step(opt)
+        opt.zero_grad(set_to_none=False)
+        return loss
+
+    for w in range(args.warmup):
+        step(w)
+    torch.cuda.synchronize()
+    probe = ConvProbe()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        loss = step(args.warmup + k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    probe.install(ops)
+    try:
+        step(999)
+    finally:
+        probe.uninstall()
+    by = probe.summary()
+    roof = None
+    if by:
+        kname = max(by, key=lambda k: by[k][1])
+        fl, ms, n = by[kname]
+        roof = {"bound": "mfma", "achieved": fl / (ms * 1e-3) / 1e12, "peak": PEAK["fp32"] / 1e12, "unit": "TFLOP/s",
+                "frac": fl / (ms * 1e-3) / PEAK["fp32"], "traffic": None, "kernel": kname,
+                "launches_per_pass": n, "avg_launch_us": ms * 1e3 / max(n, 1), "scope": "3x3 convs of the step (forward and dgrad)"}
+    line = {"metric": "consistency-training samples/s (sebridge_v3, loss mse, fp32)", "value": args.steps * B / el,
+            "unit": "samples/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32", "data": "synthetic complex spectrogram pairs; formula weights of the NCSN++ architecture",
+            "config": {"workload": (f"§8(f)2 training step: B={B} x [256, {T}] spectrogram pairs, two NCSN++ "
+                                    "evaluations + backward + fused Adam/EMA"), "global_batch": B, "per_gpu_batch": B,
+                       "seq_len": T, "parallelism": "dp1"},
+            "roofline": roof, "cpu_baseline": None, "loss": float(loss)}
+    print(json.dumps(line), flush=True)
+
+
 # ----------------------------------------------------------------------------- GPU bench
 CONFIG_DEFAULTS = {"c2": dict(batch=32, N=30, seconds=4.0, dtype="bf16"),
                    "c4": dict(batch=32, N=30, seconds=4.0, dtype="bf16"),
-                   "c5": dict(batch=1, N=200, seconds=30.0, dtype="fp32")}
+                   "c5": dict(batch=1, N=200, seconds=30.0, dtype="fp32"),
+                   "train": dict(batch=8, N=30, seconds=4.0, dtype="fp32")}
 
 
 def run(args):
@@ -469,9 +531,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1, help="GPUs (ranks); 0 = C1, the CPU plumbing case")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", choices=["c2", "c4", "c5"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c4", "c5", "train"], default="c2",
                     help="c2: PC sampler, B=32 4 s bf16 (default, the headline line); c4: one-step SNR-aligned "
-                         "path (SNRNet estimate + 1 preconditioned NFE, sebridge_v3); c5: 30 s clips, N=200, fp32")
+                         "path (SNRNet estimate + 1 preconditioned NFE, sebridge_v3); c5: 30 s clips, N=200, fp32; "
+                         "train: the consistency-training step (SURVEY §8(f) 2)")
+    ap.add_argument("--frames", type=int, default=256, help="spectrogram frames of a training sample (--config train)")
     ap.add_argument("--batch", type=int, default=None, help="utterances per GPU")
     ap.add_argument("--N", type=int, default=None, help="PC steps")
     ap.add_argument("--seconds", type=float, default=None)
@@ -493,6 +557,9 @@ def main():
         return 0
     if args.gpus == 0:
         run_c1(args)
+        return 0
+    if args.config == "train":
+        run_train(args)
         return 0
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # start the N ranks here (no torchrun); nothing in this process has touched the GPU
