@@ -48,16 +48,24 @@ def transform_mode(transform):
 
 
 class PCEnhancer:
-    """PC-sampler enhancement of a batch of noisy waveforms with an NCSNppHIP network."""
+    """PC-sampler enhancement of a batch of noisy waveforms with an NCSNppHIP network.
+
+    streams > 1 splits the batch into that many lanes, each on its own HIP stream with its own
+    GroupNorm-statistics arena and split-K workspace, and issues their network evaluations
+    alternately (sampler.pc_sample_lockstep): one lane's latency-bound low-resolution levels overlap
+    the other lane's full-resolution GEMMs.  The noise draws are the whole-batch ones (LaneNoise), so
+    the result equals the single-stream run."""
 
     def __init__(self, net, sde: sampler.SDESpec, N=30, eps=0.03, snr=0.5, predictor="reverse_diffusion",
-                 corrector="ald", corrector_steps=1, score_mode=0, transform="exponent"):
+                 corrector="ald", corrector_steps=1, score_mode=0, transform="exponent", streams=1):
         self.net, self.sde, self.N, self.eps, self.snr = net, sde, N, eps, snr
         self.mode = transform_mode(transform)
         self.predictor, self.corrector, self.corrector_steps = predictor, corrector, corrector_steps
         self.score_mode = score_mode
+        self.streams = int(streams)
+        self._lane_streams = {}
 
-    def sample(self, Y, noise: sampler.NoiseSource | None = None):
+    def _iter(self, Y, noise):
         net = self.net
 
         def step(x, tv, coef, z, seed, off):
@@ -69,9 +77,37 @@ class PCEnhancer:
         def score_tensor(x, tv):
             return net.score(x, Y, tv, self.score_mode)
 
-        return sampler.pc_sample(step, Y, self.sde, N=self.N, eps=self.eps, snr=self.snr,
-                                 predictor=self.predictor, corrector=self.corrector,
-                                 corrector_steps=self.corrector_steps, noise=noise, score_tensor=score_tensor)
+        return sampler.pc_sample_iter(step, Y, self.sde, N=self.N, eps=self.eps, snr=self.snr,
+                                      predictor=self.predictor, corrector=self.corrector,
+                                      corrector_steps=self.corrector_steps, noise=noise, score_tensor=score_tensor)
+
+    def sample(self, Y, noise: sampler.NoiseSource | None = None):
+        B = Y.shape[0]
+        noise = noise or sampler.NoiseSource()
+        nl = min(self.streams, B)
+        if nl <= 1:
+            it = self._iter(Y, noise)
+            while True:
+                try:
+                    next(it)
+                except StopIteration as e:
+                    return e.value
+        cur = torch.cuda.current_stream(Y.device)
+        bounds = [(B * h // nl, B * (h + 1) // nl) for h in range(nl)]
+        lanes = []
+        for h, (a, b) in enumerate(bounds):
+            s = self._lane_streams.get((Y.device, h))
+            if s is None:
+                s = self._lane_streams[(Y.device, h)] = torch.cuda.Stream(device=Y.device)
+            s.wait_stream(cur)
+            with torch.cuda.stream(s):
+                Yh = Y[a:b].contiguous()
+                lanes.append((s, self._iter(Yh, sampler.LaneNoise(noise, a, b, B))))
+        res = sampler.pc_sample_lockstep(lanes)
+        for (s, _), (x, _) in zip(lanes, res):
+            cur.wait_stream(s)
+            x.record_stream(cur)
+        return torch.cat([x for x, _ in res]), res[0][1]
 
     def __call__(self, y, noise=None):
         """y [B, L] f32 device -> (x_hat [B, L] f32, nfe)."""
@@ -81,7 +117,6 @@ class PCEnhancer:
         Y = ops.stft(y, 1.0, tpad=pad_frames(T), mode=self.mode, in_div=nf)
         x, nfe = self.sample(Y, noise)
         return ops.istft(x, L, mode=self.mode, out_scale=nf), nfe
-
 
 class SNRAlignedEnhancer:
     """One-step SNR-aligned enhancement of a batch (C4: model_type 'sebridge_v3',

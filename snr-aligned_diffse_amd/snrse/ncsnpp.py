@@ -121,6 +121,7 @@ class NCSNppHIP:
         self.dtype = dtype
         self.device = torch.device(device)
         self._arena = None  # ops.StatsArena of the GroupNorm statistics, one fill per evaluation
+        self._arenas = {}   # one arena per launch stream (the two-stream sampler runs evaluations concurrently)
         check_topology(**cfg)
         self.plan = build_plan(**cfg)
         dev, dt = self.device, dtype
@@ -249,9 +250,12 @@ class NCSNppHIP:
     def pyramid(self, x, y, t):
         """x, y complex64 [B,F,T] (contiguous, device); t [B] f32 -> final pyramid [B,F,T,4] f32
         (ncsnpp.py:389-398 before the division by t and the output layer)."""
-        if self._arena is None:
-            self._arena = ops.StatsArena(x.device)
-        with self._arena:
+        key = torch.cuda.current_stream(x.device).cuda_stream
+        arena = self._arenas.get(key)
+        if arena is None:
+            arena = self._arenas[key] = ops.StatsArena(x.device)
+        self._arena = arena
+        with arena:
             return self._pyramid(x, y, t)
 
     def _pyramid(self, x, y, t):

@@ -38,7 +38,12 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-_WS = {"dev": None, "buf": None}
+_WS = {"dev": None, "buf": None, "lane": 0, "bufs": {}}
+
+
+def _ws_alloc(dev):
+    mb = int(os.environ.get("SNRSE_WORKSPACE_MB", "128"))
+    return (torch.empty(mb << 18, dtype=torch.float32, device=dev) if mb > 0 else None), mb
 
 
 def _workspace(dev):
@@ -46,10 +51,25 @@ def _workspace(dev):
     (snrse_set_workspace); SNRSE_WORKSPACE_MB sizes it, 0 disables K splitting."""
     if _WS["dev"] == dev:
         return
-    mb = int(os.environ.get("SNRSE_WORKSPACE_MB", "128"))
-    buf = torch.empty(mb << 18, dtype=torch.float32, device=dev) if mb > 0 else None
+    buf, mb = _ws_alloc(dev)
     _lib.call("snrse_set_workspace", None if buf is None else buf.data_ptr(), 0 if buf is None else mb << 20)
-    _WS.update(dev=dev, buf=buf)
+    _WS.update(dev=dev, buf=buf, lane=0, bufs={0: buf})
+
+
+def use_workspace_lane(lane, dev):
+    """Point the library's split-K workspace at lane `lane`'s own buffer (allocated on first use).
+    The two-stream sampler (snrse.sampler.pc_sample_lockstep) issues each half-batch's launches
+    behind its lane's workspace, so concurrent split-K GEMMs on different streams never share one."""
+    _workspace(dev)
+    if _WS["lane"] == lane:
+        return
+    buf = _WS["bufs"].get(lane)
+    if buf is None and lane not in _WS["bufs"]:
+        buf, _ = _ws_alloc(dev)
+        _WS["bufs"][lane] = buf
+    mb = 0 if buf is None else buf.numel() * 4 >> 20
+    _lib.call("snrse_set_workspace", None if buf is None else buf.data_ptr(), mb << 20)
+    _WS.update(buf=buf, lane=lane)
 
 
 def _dev(*ts):

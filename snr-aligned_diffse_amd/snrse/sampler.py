@@ -122,6 +122,24 @@ class NoiseSource:
         return None, i * numel
 
 
+class LaneNoise(NoiseSource):
+    """The draws of batch rows [a, b) of a parent NoiseSource over the whole batch: the tape's row slice,
+    or the parent's Philox counters of those elements (offset i * numel(batch) + a * numel(row)), so a
+    half-batch run on its own stream draws exactly the numbers the whole-batch run would."""
+
+    def __init__(self, parent: NoiseSource, a, b, rows):
+        super().__init__(parent.seed, None)
+        self.parent_tape, self.a, self.b, self.rows = parent.tape, a, b, rows
+
+    def next(self, numel):
+        i = self.i
+        self.i += 1
+        if self.parent_tape is not None:
+            return self.parent_tape(i)[self.a:self.b].contiguous(), 0
+        row = numel // (self.b - self.a)
+        return None, i * row * self.rows + self.a * row
+
+
 def pc_sample(score_step, Y, sde: SDESpec, N=30, eps=0.03, snr=0.5, predictor="reverse_diffusion",
               corrector="ald", corrector_steps=1, noise: NoiseSource | None = None, denoise=True,
               score_tensor=None, Y_prior=None, probability_flow=False):
@@ -129,6 +147,43 @@ def pc_sample(score_step, Y, sde: SDESpec, N=30, eps=0.03, snr=0.5, predictor="r
     score_step(x, t_vec, coef_row, z, seed, offset) -> (x_new, x_mean) runs the network + fused step;
     score_tensor(x, t_vec) -> complex score (only needed for the Langevin corrector).
     Returns (x_result, nfe)."""
+    it = pc_sample_iter(score_step, Y, sde, N=N, eps=eps, snr=snr, predictor=predictor, corrector=corrector,
+                        corrector_steps=corrector_steps, noise=noise, denoise=denoise, score_tensor=score_tensor,
+                        Y_prior=Y_prior, probability_flow=probability_flow)
+    while True:
+        try:
+            next(it)
+        except StopIteration as e:
+            return e.value
+
+
+def pc_sample_lockstep(lanes):
+    """Run several PC loops (one per half-batch) with their launches interleaved step by step, each
+    on its own HIP stream and split-K workspace: `lanes` = [(stream, pc_sample_iter generator)].
+    While one lane's network evaluation is in its latency-bound low-resolution levels, the other
+    lane's full-resolution GEMMs fill the chip.  Returns [(x_result, nfe)] in lane order."""
+    out = [None] * len(lanes)
+    live = list(range(len(lanes)))
+    while live:
+        for k in list(live):
+            stream, it = lanes[k]
+            dev = stream.device
+            with torch.cuda.stream(stream):
+                ops.use_workspace_lane(k, dev)
+                try:
+                    next(it)
+                except StopIteration as e:
+                    out[k] = e.value
+                    live.remove(k)
+    ops.use_workspace_lane(0, lanes[0][0].device)
+    return out
+
+
+def pc_sample_iter(score_step, Y, sde: SDESpec, N=30, eps=0.03, snr=0.5, predictor="reverse_diffusion",
+                   corrector="ald", corrector_steps=1, noise: NoiseSource | None = None, denoise=True,
+                   score_tensor=None, Y_prior=None, probability_flow=False):
+    """pc_sample as a generator: yields after issuing each step (one network evaluation + its fused SDE
+    update), returns (x_result, nfe) through StopIteration."""
     noise = noise or NoiseSource()
     steps, prior, ns = build_schedule(sde, N, eps, predictor, corrector, snr, corrector_steps, probability_flow)
     B = Y.shape[0]
@@ -148,6 +203,7 @@ def pc_sample(score_step, Y, sde: SDESpec, N=30, eps=0.03, snr=0.5, predictor="r
             z, off = noise.next(numel)
             x, x_mean = score_step(x, tv, ctab[ci], z, noise.seed, off)
             ci += 1
+            yield
         elif kind == "langevin":
             grad = score_tensor(x, tv)
             z, off = noise.next(numel)
@@ -159,6 +215,7 @@ def pc_sample(score_step, Y, sde: SDESpec, N=30, eps=0.03, snr=0.5, predictor="r
             e = (snr * nn_ / gn) ** 2 * 2
             row = torch.stack([torch.ones_like(e), torch.zeros_like(e), e, torch.sqrt(e * 2)]).float()
             x, x_mean = ops.sde_update(x, row.expand(B, 4).contiguous(), score=grad, noise=z)
+            yield
         else:  # NonePredictor
             x_mean = x
     return (x_mean if denoise else x), ns
