@@ -964,39 +964,6 @@ SNRSE_DEV void epilogue_swapped(const ConvParams& p, const f32x4 (&acc)[2][4][4]
   }
 }
 
-// GroupNorm prologue of the v5 halo kernel on one 16-B vector (8 bf16 channels): GNM 1 = affine,
-// 2 = affine + SiLU; `ok` = inside the image (else the conv's zero padding).  Written stage by stage
-// over the 8 elements (8 independent exp / rcp chains) so the schedule can hide the transcendental
-// latencies; element by element the chain was fully serial with an s_nop after every exp and rcp.
-template <int GNM>
-SNRSE_DEV u32x4 gn_xform8(const u32x4 v, const float* sc, const float* sh, bool ok) {
-  float y[8];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    y[2 * i] = fmaf(__uint_as_float(v[i] << 16), sc[2 * i], sh[2 * i]);
-    y[2 * i + 1] = fmaf(__uint_as_float(v[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]);
-  }
-  if constexpr (GNM == 2) {
-    // sched_barrier(0) between the stages: without it the scheduler (at the kernel's 256-VGPR limit)
-    // re-serialises the 8 chains to save registers
-    float e[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_exp2f(y[k] * -1.44269504088896341f);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_rcpf(1.0f + e[k]);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) y[k] *= e[k];
-  }
-  // zero padding as an AND mask: a select here becomes an exec-masked branch around the whole transform
-  const uint32_t okm = 0u - (uint32_t)ok;
-  u32x4 o;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = pack_bf16x2(y[2 * i], y[2 * i + 1]) & okm;
-  return o;
-}
-
 template <typename TO, int GNM, int EF>
 __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   constexpr bool H5SW = SNRSE_H5_SWAP && sizeof(TO) == 2;  // swapped operands + register epilogue

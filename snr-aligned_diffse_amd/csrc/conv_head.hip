@@ -47,7 +47,8 @@ SNRSE_DEV int kh_swz(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >
     }                                                                                                          \
   } while (0)
 
-// grid: B * (H / 4) * (W / 64) workgroups of 256
+// grid: B * (H / 4) * (W / 64) workgroups of 256.  GNM: 0 no prologue, 1 GroupNorm affine, 2 + SiLU
+template <int GNM>
 __global__ __launch_bounds__(256) void conv_head_kernel(ConvParams p) {
   __shared__ __attribute__((aligned(16))) char smem[KH_LDS];
   char* const halo = smem;
@@ -64,7 +65,7 @@ __global__ __launch_bounds__(256) void conv_head_kernel(ConvParams p) {
   const int nc = Cin >> 5;
   const int K1 = 9 * Cin;
   const int hcol = tid & 3;
-  const bool gn = p.gn_scale != nullptr;
+  constexpr bool gn = GNM > 0;
   const int lrow = lane & 15, lg = lane >> 4;
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.wgt, p.wbytes);
 
@@ -93,19 +94,10 @@ __global__ __launch_bounds__(256) void conv_head_kernel(ConvParams p) {
       const int hr = (tid >> 2) + 64 * j;
       if (j == KH_HJ - 1 && hr >= KH_HROWS) break;
       u32x4 v = hv[j];
-      if (gn) {
+      if constexpr (gn) {
         const float sc[8] = {gs0[0], gs0[1], gs0[2], gs0[3], gs1[0], gs1[1], gs1[2], gs1[3]};
         const float sh[8] = {gh0[0], gh0[1], gh0[2], gh0[3], gh1[0], gh1[1], gh1[2], gh1[3]};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float lo = fmaf(__uint_as_float(v[i] << 16), sc[2 * i], sh[2 * i]);
-          float hi = fmaf(__uint_as_float(v[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]);
-          if (p.gn_act) {
-            lo = silu(lo);
-            hi = silu(hi);
-          }
-          v[i] = hok[j] ? pack_bf16x2(lo, hi) : 0u;
-        }
+        v = gn_xform8<GNM>(v, sc, sh, hok[j]);  // rows outside the image: the conv's zero padding
       }
       *(u32x4*)(halo + kh_swz(hr, hcol)) = v;
     }
@@ -161,7 +153,9 @@ int launch_head(const ConvParams& p, hipStream_t s) {
   if (!head_ok(p)) return SNRSE_EINVAL;
   const long long tiles = (long long)p.B * (p.H / KH_TH) * (p.W / KH_TW);
   if (tiles <= 0 || tiles > 0x7fffffffLL) return SNRSE_EINVAL;
-  hipLaunchKernelGGL(conv_head_kernel, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  if (!p.gn_scale) hipLaunchKernelGGL(conv_head_kernel<0>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  else if (!p.gn_act) hipLaunchKernelGGL(conv_head_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(conv_head_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, s, p);
   return (int)hipGetLastError();
 }
 
