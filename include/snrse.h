@@ -92,7 +92,8 @@ int snrse_gn_apply(const void* src0, int C0, const void* src1, int C1, int B, in
 /* LDS-tiled GroupNorm-apply + SiLU + FIR x2 of a ResBlock with up/down (layerspp.py:245-257), bf16:
  * out_act = FIR(act(x*scale+shift)) and, when out_raw != NULL, out_raw = FIR(x) (the shortcut input,
  * layerspp.py:249/255), both [B][Ho][Wo][C] from one pass over x.  scale/shift [B][C] f32 from
- * snrse_gn_scale_shift, or both NULL (identity).  mode 1 down (H, W even), 2 up.  C % 16 == 0. */
+ * snrse_gn_scale_shift, or both NULL (identity).  mode 1 down (H, W even), 2 up.  C % 8 == 0 with C / 8
+ * dividing 64 (the row-strip kernel), otherwise C % 16 == 0 (the LDS-tiled kernel). */
 int snrse_gn_resample(const void* src, int C, int B, int H, int W, const float* scale, const float* shift,
                       int act, int mode, void* out_act, void* out_raw, hipStream_t stream);
 
@@ -104,21 +105,26 @@ int snrse_gn_act(const void* src0, int C0, const void* src1, int C1, int B, int 
 /* Split-K workspace of the small-image conv GEMMs (levels whose tile grid underfills the CUs): a
  * device buffer of `bytes` the caller keeps alive and leaves untouched while convs run; the library
  * keeps [splits][M][Cout] f32 partial sums there and splits only when they fit.  NULL disables
- * splitting (the default).  One workspace per process: convs using it must share one stream. */
+ * splitting (the default).  The pointer is captured when a conv is launched: launches that may run
+ * concurrently (different streams) must be issued behind different workspaces (snrse.ops
+ * use_workspace_lane does this for the two-stream sampler). */
 int snrse_set_workspace(void* ptr, size_t bytes);
 
-/* Tuning switches (A/B experiments): "conv_variant" 0 auto, 1 register-staged v1, 2 LDS-DMA v2,
- * 4 halo kernel v4 with the register epilogue, 5 halo kernel v5 (two workgroups per CU), 6
- * persistent halo v6, 8 ping-pong halo v8 (6 / 8 fall back to 4 / 5 outside their contract);
- * "splitk" 0 disables the split-K small-image GEMMs; "stats_zeroed" 1 = the statistics buffers
- * handed to snrse_conv2d / snrse_gn_stats are already zero (the caller clears one arena per network
- * evaluation), so they skip their per-call memset. */
+/* Tuning switches (A/B experiments; the Python host also reads SNRSE_OPTS="name=value,..." at load):
+ * "conv_variant" 0 auto, 1 register-staged v1, 2 LDS-DMA v2, 5 halo GEMM v5 (the default halo kernel);
+ * "splitk" 0 disables the split-K small-image GEMMs, "splitk_target" workgroups a split launch aims for;
+ * "epi_nt" 0 / 1 / 2 (auto above 256 MB of output) non-temporal halo-GEMM output stores;
+ * "h5_specialise" 1 compile-time epilogue flags for the NCSN++ ResBlock configurations;
+ * "h5_persist" / "h5_stagger" persistent staggered halo launches (measured slower: off);
+ * "resample_variant" 0 row-strip / 1 LDS-tiled gn_resample, "resample_nt" non-temporal stores there;
+ * "stats_zeroed" 1 = the statistics buffers handed to snrse_conv2d / snrse_gn_stats are already zero (the
+ * caller clears one arena per network evaluation), so they skip their per-call memset. */
 int snrse_set_option(const char* name, int value);
 
-/* Read back a switch: "conv_variant", "splitk", "stats_zeroed", "halo_kernel" = generation of the halo conv kernel
- * the current setting dispatches to (4, 5, 6, 8), "last_kernel" = generation of the most recent
- * snrse_conv2d launch (1 v1, 2 v2, 4/5/6/8 halo, 9 pyramid head), "last_ksplit" = K splits of the
- * most recent v2 launch. */
+/* Read back a switch (any name above) or: "halo_kernel" = generation of the halo conv kernel the current
+ * setting dispatches to (5), "last_kernel" = generation of the most recent snrse_conv2d launch (1 v1, 2 v2,
+ * 5 halo, 10 pyramid head), "last_ksplit" = K splits of the most recent v2 launch, "last_epi_nt" /
+ * "last_chunks" = store flavour / image-range launches of the most recent halo conv. */
 int snrse_get_option(const char* name, int* value);
 
 /* AttnBlockpp attention core (layerspp.py:84-88): qkv [B][L][3C] -> out [B][L][C],

@@ -1514,6 +1514,7 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   }
   if (name_is(name, "last_kernel")) { *value = g_last_kernel; return 0; }
   if (name_is(name, "splitk")) { *value = g_splitk; return 0; }
+  if (name_is(name, "splitk_target")) { *value = g_splitk_target; return 0; }
   if (name_is(name, "h5_persist")) { *value = g_h5_persist; return 0; }
   if (name_is(name, "epi_nt")) { *value = g_epi_nt; return 0; }
   if (name_is(name, "h5_stagger")) { *value = g_h5_stagger_per_phase; return 0; }
