@@ -520,6 +520,9 @@ def run(args):
             "roofline": roof, "cpu_baseline": cpu,
             "output_rms_mean": float(allm.mean()),
         }
+        if sdist.oversubscribed(world):  # a launcher rehearsal: ranks share the visible GPU(s)
+            line["oversubscribed"] = {"ranks": world, "devices": torch.cuda.device_count(),
+                                      "note": "ranks share devices; collectives on gloo; not a scaling figure"}
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

@@ -11,12 +11,23 @@ import torch
 import torch.distributed as dist
 
 
+def oversubscribed(world: int) -> bool:
+    """More ranks than visible GPUs (a rehearsal of the N-rank launch on a smaller box): ranks then
+    share devices round-robin and the collectives run on gloo (RCCL needs one rank per device).
+    torch.cuda.device_count() does not initialise the GPU."""
+    n = torch.cuda.device_count()
+    return 0 < n < world
+
+
 def init_from_env(backend: str | None = None):
     """(rank, world, device) from torchrun's env; single process skips process-group init."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = torch.cuda.is_available() and backend != "gloo"
+    if use_gpu and oversubscribed(world):
+        local %= torch.cuda.device_count()
+        backend = backend or "gloo"
     dev = torch.device("cuda", local) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(local)
@@ -36,10 +47,15 @@ def shard_range(n: int, rank: int, world: int):
     return start, start + base + (1 if rank < extra else 0)
 
 
+def _coll_device(device):
+    """gloo collectives take host tensors."""
+    return torch.device("cpu") if dist.get_backend() == "gloo" else device
+
+
 def max_over_ranks(value: float, device) -> float:
     if not (dist.is_available() and dist.is_initialized()):
         return float(value)
-    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t)
 
@@ -52,6 +68,8 @@ def gather_metrics(values, n_total: int, rank: int, world: int, device):
         vals = vals[:, None]
     if not (dist.is_available() and dist.is_initialized()) or world == 1:
         return vals
+    out_dev, device = device, _coll_device(device)
+    vals = vals.to(device)
     k = vals.shape[1]
     cap = shard_range(n_total, 0, world)[1]  # largest shard
     pad = torch.full((cap, k), float("nan"), dtype=torch.float64, device=device)
@@ -62,7 +80,7 @@ def gather_metrics(values, n_total: int, rank: int, world: int, device):
     for r in range(world):
         a, b = shard_range(n_total, r, world)
         rows.append(bufs[r][: b - a])
-    return torch.cat(rows, 0)
+    return torch.cat(rows, 0).to(out_dev)
 
 
 def free_port() -> int:
