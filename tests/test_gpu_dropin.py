@@ -16,6 +16,15 @@ def rel(a, b):
     return float((a - b).abs().pow(2).mean().sqrt() / (b.abs().pow(2).mean().sqrt() + 1e-30))
 
 
+def abs_rms(a, b):
+    """Absolute RMS error over the complex elements (the north star's "1e-4 RMS on the complex
+    spectrogram"; rel() divides it by the golden's RMS, ~3.5 for the network / PC goldens)."""
+    a = torch.as_tensor(a).detach().cpu()
+    b = torch.as_tensor(b).detach().cpu()
+    dt = torch.complex128 if (a.is_complex() or b.is_complex()) else torch.float64
+    return float((a.to(dt) - b.to(dt)).abs().pow(2).mean().sqrt())
+
+
 def score_model(model_type="bbed", snr_conditioned="false", dtype="fp32", **kw):
     from sgmse.model import ScoreModel
     hp = dict(backbone="ncsnpp", sde="ouve", model_type=model_type, snr_conditioned=snr_conditioned, theta=1.5,
@@ -39,6 +48,7 @@ def test_pc_sampler_golden(gpu):
     x, ns = sampler()
     assert ns == 10 and x.shape == Y.shape
     assert rel(x, g["out"]) < 1e-4
+    assert abs_rms(x, g["out"]) < 1e-4  # the north star's absolute bound on the complex spectrogram
 
 
 def test_forward_preconditioning(gpu):
