@@ -1497,7 +1497,7 @@ extern "C" int snrse_debug_set_stamps(void* buf) {
 }
 #endif
 
-extern __attribute__((visibility("hidden"))) int g_resample_variant, g_resample_nt;  // resample.hip
+extern __attribute__((visibility("hidden"))) int g_resample_variant, g_resample_nt, g_resample_down_rows;  // resample.hip
 
 static bool name_is(const char* a, const char* b) {
   int i = 0;
@@ -1525,6 +1525,7 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   if (name_is(name, "last_chunks")) { *value = g_last_chunks; return 0; }
   if (name_is(name, "resample_variant")) { *value = g_resample_variant; return 0; }
   if (name_is(name, "resample_nt")) { *value = g_resample_nt; return 0; }
+  if (name_is(name, "resample_down_rows")) { *value = g_resample_down_rows; return 0; }
   return SNRSE_EINVAL;
 }
 
@@ -1540,6 +1541,7 @@ extern "C" int snrse_set_option(const char* name, int value) {
   if (name_is(name, "stats_zeroed")) { g_snrse_stats_zeroed = value ? 1 : 0; return 0; }
   if (name_is(name, "resample_variant")) { g_resample_variant = value; return 0; }
   if (name_is(name, "resample_nt")) { g_resample_nt = value; return 0; }
+  if (name_is(name, "resample_down_rows")) { g_resample_down_rows = value; return 0; }
   return SNRSE_EINVAL;
 }
 

@@ -17,6 +17,7 @@
 
 // option "resample_variant" (snrse_set_option): 0 auto (row strips where C / 8 divides 64), 1 tiled
 __attribute__((visibility("hidden"))) int g_resample_variant = 0;
+__attribute__((visibility("hidden"))) int g_resample_down_rows = 2;  // option "resample_down_rows": output rows per down strip (1, 2, 4)
 // option "resample_nt": 1 = non-temporal stores in the row-strip kernel
 __attribute__((visibility("hidden"))) int g_resample_nt = 0;
 
@@ -238,7 +239,8 @@ __global__ __launch_bounds__(256) void gn_act_kernel(const bf16_t* __restrict__ 
 // pixel are adjacent, so each wave instruction moves 64 / NV whole pixels (full 128-B lines).  The
 // separable FIR [1,3,3,1] runs in registers: the vertical taps per input column (act and raw), then the
 // horizontal taps over a sliding window of column values.  The GroupNorm + SiLU of an input vector is
-// recomputed by each output row that reads it (2x down, 4x up; VALU, not bytes).
+// recomputed by each strip that reads it (down: (2 RD + 2) / RD x for strips of RD output rows, 1.5x at
+// the default RD = 2; up: 4x; VALU, not bytes).
 //   down: out(oy, ox) = sum_ab k[a] k[b] x(2oy-1+a, 2ox-1+b), k = [1,3,3,1]/8
 //   up:   out(2p+i, 2q+j) from input rows {p-1, p} (i = 0) or {p, p+1} (i = 1) with weights (1/4, 3/4) /
 //         (3/4, 1/4), and the same in columns: out(.., 2q) = (V(q-1) + 3 V(q)) / 4, out(.., 2q+1) =
@@ -280,7 +282,10 @@ SNRSE_DEV __amdgpu_buffer_rsrc_t rs_rsrc(const void* base, unsigned bytes) {
 // Strips are numbered per image up to a multiple of the strips of one wave (64 / NV), so a wave never
 // straddles two images: the image base is wave-uniform (one buffer resource, 32-bit offsets, hardware
 // zero-fill of out-of-image vectors).  NV lanes (CPT channels each) cover one pixel, C = NV * CPT.
-template <int MODE, int NV, int CPT>
+// RD (down only): output rows per strip.  A strip of RD rows reads 2 RD + 2 input rows, so each input
+// vector's GroupNorm + SiLU is evaluated (2 RD + 2) / RD times instead of 4 (the kernel's VALU) and each
+// input row is fetched by fewer strips (L2 traffic).
+template <int MODE, int NV, int CPT, int RD = 1>
 __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __restrict__ src, int H, int W, int L,
                                                                int nseg, int nrows, const float* __restrict__ scale,
                                                                const float* __restrict__ shift, int act,
@@ -299,7 +304,8 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
   const int ls = gs - b * sp_img;  // strip within the image
   if (b >= B || ls >= nrows * nseg) return;  // padding strips
   const int seg = ls % nseg;
-  const int orow = ls / nseg;  // output row
+  static_assert(MODE == MODE_DOWN || RD == 1, "multi-row strips: down only");
+  const int orow = (ls / nseg) * RD;  // (first) output row
   const int Ho = MODE == MODE_DOWN ? H / 2 : 2 * H, Wo = MODE == MODE_DOWN ? W / 2 : 2 * W;
   float sc[CPT], sh[CPT];
 #pragma unroll
@@ -308,12 +314,13 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
     sh[i] = scale ? shift[(size_t)b * C + CPT * v + i] : 0.f;
   }
   const __amdgpu_buffer_rsrc_t rsrc = rs_rsrc(src + (size_t)b * H * W * C, (unsigned)((size_t)H * W * C * 2));
-  constexpr int NR = MODE == MODE_DOWN ? 4 : 2;  // input rows per output row
+  constexpr int NR = MODE == MODE_DOWN ? 2 * RD + 2 : 2;  // input rows of the strip's RD output rows
   int iy0;
   float wy[NR];
   if constexpr (MODE == MODE_DOWN) {
     iy0 = 2 * orow - 1;
-    wy[0] = 0.125f; wy[1] = 0.375f; wy[2] = 0.375f; wy[3] = 0.125f;
+#pragma unroll
+    for (int a = 0; a < NR; ++a) wy[a] = 0.f;  // unused in down mode (per-row tap weights below)
   } else {
     const int p = orow >> 1;
     iy0 = (orow & 1) ? p : p - 1;
@@ -339,6 +346,35 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
     }
     return rw;
   };
+  // down: column values of the RD output rows (row rr takes input rows 2 rr .. 2 rr + 3 of the strip
+  // with the vertical taps [1,3,3,1]/8); each input vector is transformed once
+  auto eval_cols = [&](const Raw& rw, int ix, RowVec<CPT> (&cv)[RD]) {
+    const bool colok = ix >= 0 && ix < W;
+    constexpr float kv[4] = {0.125f, 0.375f, 0.375f, 0.125f};
+#pragma unroll
+    for (int rr = 0; rr < RD; ++rr)
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) { cv[rr].a[i] = 0.f; cv[rr].r[i] = 0.f; }
+#pragma unroll
+    for (int a = 0; a < NR; ++a) {
+      float x[CPT];
+      V::unpack(rw.x[a], x);
+      const bool ok = colok && rowok[a];
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) {
+        const float y = fmaf(x[i], sc[i], sh[i]);
+        const float t = ok ? (act ? silu(y) : y) : 0.f;
+#pragma unroll
+        for (int rr = 0; rr < RD; ++rr) {
+          const int k = a - 2 * rr;
+          if (k >= 0 && k < 4) {
+            cv[rr].a[i] = fmaf(t, kv[k], cv[rr].a[i]);
+            cv[rr].r[i] = fmaf(x[i], kv[k], cv[rr].r[i]);
+          }
+        }
+      }
+    }
+  };
   auto eval_col = [&](const Raw& rw, int ix) {
     const bool colok = ix >= 0 && ix < W;
     RowVec<CPT> cv;
@@ -360,8 +396,8 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
     return cv;
   };
   auto column = [&](int ix) { return eval_col(load_col(ix), ix); };
-  auto store = [&](int ox, const float* a, const float* r) {
-    const size_t o = (((size_t)b * Ho + orow) * Wo + ox) * C + CPT * v;
+  auto store = [&](int ox, const float* a, const float* r, int rr = 0) {
+    const size_t o = (((size_t)b * Ho + orow + rr) * Wo + ox) * C + CPT * v;
     if (nt) {
       __builtin_nontemporal_store(V::pack(a), (typename V::T*)(out_act + o));
       if (out_raw) __builtin_nontemporal_store(V::pack(r), (typename V::T*)(out_raw + o));
@@ -375,14 +411,18 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
     // out(ox) = k0 V(2ox-1) + k1 V(2ox) + k1 V(2ox+1) + k0 V(2ox+2): carry only the partial sum of the
     // two columns shared with the previous output
     const int ox0 = seg * L, ox1 = min(Wo, ox0 + L);
-    float pa[CPT], pr[CPT];
+    float pa[RD][CPT], pr[RD][CPT];
     {
-      const RowVec<CPT> c0 = column(2 * ox0 - 1), c1 = column(2 * ox0);
+      RowVec<CPT> c0[RD], c1[RD];
+      eval_cols(load_col(2 * ox0 - 1), 2 * ox0 - 1, c0);
+      eval_cols(load_col(2 * ox0), 2 * ox0, c1);
 #pragma unroll
-      for (int i = 0; i < CPT; ++i) {
-        pa[i] = 0.125f * c0.a[i] + 0.375f * c1.a[i];
-        pr[i] = 0.125f * c0.r[i] + 0.375f * c1.r[i];
-      }
+      for (int rr = 0; rr < RD; ++rr)
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+          pa[rr][i] = 0.125f * c0[rr].a[i] + 0.375f * c1[rr].a[i];
+          pr[rr][i] = 0.125f * c0[rr].r[i] + 0.375f * c1[rr].r[i];
+        }
     }
     Raw n2 = load_col(2 * ox0 + 1), n3 = load_col(2 * ox0 + 2);
     for (int ox = ox0; ox < ox1; ++ox) {
@@ -391,16 +431,21 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
         n2 = load_col(2 * ox + 3);
         n3 = load_col(2 * ox + 4);
       }
-      const RowVec<CPT> c2 = eval_col(r2, 2 * ox + 1), c3 = eval_col(r3, 2 * ox + 2);
-      float oa[CPT], orw[CPT];
+      RowVec<CPT> c2[RD], c3[RD];
+      eval_cols(r2, 2 * ox + 1, c2);
+      eval_cols(r3, 2 * ox + 2, c3);
 #pragma unroll
-      for (int i = 0; i < CPT; ++i) {
-        oa[i] = fmaf(0.125f, c3.a[i], fmaf(0.375f, c2.a[i], pa[i]));
-        orw[i] = fmaf(0.125f, c3.r[i], fmaf(0.375f, c2.r[i], pr[i]));
-        pa[i] = fmaf(0.375f, c3.a[i], 0.125f * c2.a[i]);
-        pr[i] = fmaf(0.375f, c3.r[i], 0.125f * c2.r[i]);
+      for (int rr = 0; rr < RD; ++rr) {
+        float oa[CPT], orw[CPT];
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+          oa[i] = fmaf(0.125f, c3[rr].a[i], fmaf(0.375f, c2[rr].a[i], pa[rr][i]));
+          orw[i] = fmaf(0.125f, c3[rr].r[i], fmaf(0.375f, c2[rr].r[i], pr[rr][i]));
+          pa[rr][i] = fmaf(0.375f, c3[rr].a[i], 0.125f * c2[rr].a[i]);
+          pr[rr][i] = fmaf(0.375f, c3[rr].r[i], 0.125f * c2[rr].r[i]);
+        }
+        store(ox, oa, orw, rr);
       }
-      store(ox, oa, orw);
     }
   } else {
     // output columns 2q, 2q+1 for input columns q in [q0, q1)
@@ -427,10 +472,10 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
   }
 }
 
-template <int MODE, int NV, int CPT>
+template <int MODE, int NV, int CPT, int RD = 1>
 int launch_rows(const void* src, int B, int H, int W, const float* scale, const float* shift, int act, void* out_act,
                 void* out_raw, hipStream_t stream) {
-  const int nrows = MODE == MODE_DOWN ? H / 2 : 2 * H;
+  const int nrows = MODE == MODE_DOWN ? H / 2 / RD : 2 * H;  // strips per column segment
   const int span = MODE == MODE_DOWN ? W / 2 : W;  // positions a strip walks (output cols / input cols)
   // strip length: 16 positions, shortened on small images until the grid has >= 2^17 threads (8 waves
   // per CU)
@@ -442,7 +487,7 @@ int launch_rows(const void* src, int B, int H, int W, const float* scale, const 
   const long long nblk = (sp_img * B + SPB - 1) / SPB;
   if (nblk > 0x7fffffffLL || sp_img * B > 0x7fffffffLL || (long long)H * W * NV * CPT * 2 >= 0x7fffffffLL)
     return SNRSE_EINVAL;
-  hipLaunchKernelGGL((gn_resample_rows_kernel<MODE, NV, CPT>), dim3((unsigned)nblk), dim3(256), 0, stream,
+  hipLaunchKernelGGL((gn_resample_rows_kernel<MODE, NV, CPT, RD>), dim3((unsigned)nblk), dim3(256), 0, stream,
                      (const bf16_t*)src, H, W, L, nseg, nrows, scale, shift, act, (bf16_t*)out_act, (bf16_t*)out_raw,
                      (int)nblk, B, (int)sp_img, g_resample_nt);
   return (int)hipGetLastError();
@@ -450,21 +495,33 @@ int launch_rows(const void* src, int B, int H, int W, const float* scale, const 
 
 // down: 4 channels per lane (8 input vectors per output column pair stay within 4 waves per SIMD);
 // up: 8 channels per lane (16-B stores)
-template <int MODE>
-int dispatch_rows(const void* src, int C, int B, int H, int W, const float* scale, const float* shift, int act,
-                  void* out_act, void* out_raw, hipStream_t stream) {
+template <int MODE, int RD>
+int dispatch_rows_rd(const void* src, int C, int B, int H, int W, const float* scale, const float* shift, int act,
+                     void* out_act, void* out_raw, hipStream_t stream) {
   constexpr int CPT = MODE == MODE_DOWN ? 4 : 8;
   if (C % CPT) return -1;
   switch (C / CPT) {
-    case 1: return launch_rows<MODE, 1, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
-    case 2: return launch_rows<MODE, 2, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
-    case 4: return launch_rows<MODE, 4, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
-    case 8: return launch_rows<MODE, 8, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
-    case 16: return launch_rows<MODE, 16, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
-    case 32: return launch_rows<MODE, 32, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
-    case 64: return launch_rows<MODE, 64, CPT>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 1: return launch_rows<MODE, 1, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 2: return launch_rows<MODE, 2, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 4: return launch_rows<MODE, 4, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 8: return launch_rows<MODE, 8, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 16: return launch_rows<MODE, 16, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 32: return launch_rows<MODE, 32, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 64: return launch_rows<MODE, 64, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
     default: return -1;  // not handled here
   }
+}
+template <int MODE>
+int dispatch_rows(const void* src, int C, int B, int H, int W, const float* scale, const float* shift, int act,
+                  void* out_act, void* out_raw, hipStream_t stream) {
+  if constexpr (MODE == MODE_DOWN) {
+    const int Ho = H / 2;
+    if (g_resample_down_rows >= 4 && Ho % 4 == 0)
+      return dispatch_rows_rd<MODE, 4>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    if (g_resample_down_rows >= 2 && Ho % 2 == 0)
+      return dispatch_rows_rd<MODE, 2>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream);
+  }
+  return dispatch_rows_rd<MODE, 1>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream);
 }
 
 template <int MODE>

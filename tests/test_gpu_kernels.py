@@ -608,3 +608,35 @@ def test_input_conv_fused_vs_im2col_gemm(gpu):
     assert (h.float().cpu() - ref).abs().max().item() <= 2 ** -7 * ref.abs().max().item()
     ok_shape = torch.zeros(1, 8, 64, dtype=torch.complex64, device=gpu)
     assert not ops.input_conv_ok(ok_shape)  # 8 x 64 px = 8 tiles: outside the contract
+
+
+@pytest.mark.parametrize("shape", [(2, 128, 8, 16), (1, 256, 36, 70), (3, 16, 18, 34), (2, 128, 64, 256),
+                                   (1, 512, 6, 40), (2, 8, 8, 8), (1, 64, 20, 12)])
+def test_gn_resample_down_rows(gpu, shape):
+    """Down-sampling row strips of 1, 2 and 4 output rows (option "resample_down_rows"; a strip of RD
+    rows reads 2 RD + 2 input rows and transforms each once): the same per-output fmaf sequence, so
+    the three are bit-identical, and all match the oracle FIR of an fp64 GroupNorm+SiLU
+    (layerspp.py:245-257, up_or_down_sampling.py:195-257).  Heights with H/2 not divisible by RD fall
+    back to fewer rows per strip."""
+    from snrse import ops
+    B, C, H, W = shape
+    x = (torch.from_numpy(fnormal("t.rs.x", (B, C, H, W))) * 2 + 0.3).bfloat16().float()
+    g = torch.from_numpy(fnormal("t.rs.g", (C,))) * 0.1 + 1
+    be = torch.from_numpy(fnormal("t.rs.b", (C,))) * 0.1
+    ref_a = ncsnpp_ref.fir_down2(F.silu(F.group_norm(x.double(), min(C // 4, 32), g.double(), be.double(), eps=1e-6)))
+    ref_r = ncsnpp_ref.fir_down2(x.double())
+    xg = nhwc(x).to(gpu, torch.bfloat16)
+    sums, _ = ops.gn_stats(xg)
+    scale, shift = ops.gn_scale_shift(sums, g.to(gpu), be.to(gpu), H * W)
+    old = ops.get_option("resample_down_rows")
+    outs = {}
+    try:
+        for rd in (1, 2, 4):
+            ops.set_option("resample_down_rows", rd)
+            outs[rd] = ops.gn_resample(xg, scale, shift, act=True, mode="down", want_raw=True)
+    finally:
+        ops.set_option("resample_down_rows", old)
+    for rd, (a, r) in outs.items():
+        assert rel(nchw(a.float()), ref_a) < 1e-2, rd
+        assert rel(nchw(r.float()), ref_r) < 1e-2, rd
+        assert torch.equal(a, outs[1][0]) and torch.equal(r, outs[1][1]), rd

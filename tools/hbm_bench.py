@@ -40,7 +40,9 @@ def main():
     ap.add_argument("--only", default="down,up,input,act")
     ap.add_argument("--resample-variant", type=int, default=0)
     ap.add_argument("--nt", type=int, default=0)
+    ap.add_argument("--down-rows", type=int, default=2, help="option resample_down_rows (1, 2, 4)")
     a = ap.parse_args()
+    ops.set_option("resample_down_rows", a.down_rows)
     ops.set_option("resample_variant", a.resample_variant)
     ops.set_option("resample_nt", a.nt)
     dev = torch.device("cuda")
@@ -60,7 +62,7 @@ def main():
             ms = timed(lambda: ops.gn_resample(x, sc, sh, act=True, mode=kind, want_raw=True), a.reps)
             f = 0.25 if kind == "down" else 4.0
             byt = x.numel() * 2 * (1 + 2 * f)
-            rows.append({"kernel": f"gn_resample_{kind}", "variant": a.resample_variant, "shape": [B, H, W, C], "us": ms * 1e3,
+            rows.append({"kernel": f"gn_resample_{kind}", "variant": a.resample_variant, "down_rows": a.down_rows, "shape": [B, H, W, C], "us": ms * 1e3,
                          "bytes": byt, "TBps": byt / ms / 1e9})
             tot.setdefault(kind, [0.0, 0.0])
             tot[kind][0] += byt
