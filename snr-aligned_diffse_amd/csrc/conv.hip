@@ -978,6 +978,10 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const halo = smem;
   char* const ring = smem + HALO_BYTES;
+  // GroupNorm scale / shift of the next chunk's 32 channels (2 x 32 f32), written by the first 16
+  // lanes of wave 0 before the chunk-end barrier and read by every thread's halo transform, so no
+  // thread keeps them in registers across the MFMA phases
+  float* const gnl = (float*)(smem + HALO_BYTES + 2 * SLOT + 1024);  // past the stamps build's area
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1047,7 +1051,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   }
 
   u32x4 hv[HJ];
-  float gsc[8], gsh[8];
+  f32x4 gnv;  // lanes 0..15 of wave 0: 4 of the next chunk's 64 GroupNorm scale / shift values
 
 #define SNRSE_HALO5_LOADS(BASE_, BYTES_, CS_, CC_)                                                     \
   do {                                                                                              \
@@ -1064,12 +1068,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
       if (ch < p.C0) SNRSE_HALO5_LOADS(p.src0, p.bytes0, p.C0, ch);
       else SNRSE_HALO5_LOADS(p.src1, p.bytes1, p.C1, ch - p.C0);
       if constexpr (GNM > 0) {
-        const float* sp = p.gn_scale + (size_t)bb * Cin + ch + hcol * 8;
-        const float* hp = p.gn_shift + (size_t)bb * Cin + ch + hcol * 8;
-        const f32x4 s0 = *(const f32x4*)sp, s1 = *(const f32x4*)(sp + 4);
-        const f32x4 t0 = *(const f32x4*)hp, t1 = *(const f32x4*)(hp + 4);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { gsc[i] = s0[i]; gsc[4 + i] = s1[i]; gsh[i] = t0[i]; gsh[4 + i] = t1[i]; }
+        if (tid < 16) gnv = *(const f32x4*)((tid < 8 ? p.gn_scale : p.gn_shift) + (size_t)bb * Cin + ch + (tid & 7) * 4);
       }
     } else {
       const int ch = (c - cbm) * KT;
@@ -1078,8 +1077,22 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
     }
   };
 #undef SNRSE_HALO5_LOADS
+  auto gn_publish = [&]() {  // before the barrier that precedes halo_store
+    if constexpr (GNM > 0) {
+      if (tid < 16) *(f32x4*)(gnl + tid * 4) = gnv;
+    }
+  };
   auto halo_store = [&](int c) {
     const bool tr = GNM > 0 && c < cbm;
+    float gsc[8], gsh[8];
+    if constexpr (GNM > 0) {
+      if (tr) {
+        const f32x4 s0 = *(const f32x4*)(gnl + hcol * 8), s1 = *(const f32x4*)(gnl + hcol * 8 + 4);
+        const f32x4 t0 = *(const f32x4*)(gnl + 32 + hcol * 8), t1 = *(const f32x4*)(gnl + 32 + hcol * 8 + 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { gsc[i] = s0[i]; gsc[4 + i] = s1[i]; gsh[i] = t0[i]; gsh[4 + i] = t1[i]; }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < HJ; ++j) {
       const int hr = (tid >> 2) + 64 * j;
@@ -1123,6 +1136,10 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 
   halo_load(0);
   wload(0);
+  if constexpr (GNM > 0) {
+    gn_publish();
+    __syncthreads();
+  }
   halo_store(0);
   SNRSE_STAMP(1);
   const int lrow = lane & 15, lg = lane >> 4;
@@ -1169,8 +1186,9 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
     }
     SNRSE_STAMP(3 + 2 * (q & 15));
     if (last && c + 1 < ncb) {
+      gn_publish();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // every wave is done reading halo(c)
+      __builtin_amdgcn_s_barrier();  // every wave is done reading halo(c); chunk c+1's GN affine is in LDS
       halo_store(c + 1);
     }
   }
@@ -1239,11 +1257,8 @@ int launch_halo5_ef(ConvParams p, int grid, size_t lds, hipStream_t s) {
 
 template <typename TO, int GNM>
 int launch_halo5_gn(ConvParams p, hipStream_t s) {
-#ifdef SNRSE_STAMPS
-  constexpr size_t lds = 396 * 64 + 2 * 3 * 128 * 64 + 4 * 32 * 8;
-#else
-  constexpr size_t lds = 396 * 64 + 2 * 3 * 128 * 64;
-#endif
+  // halo + weight ring + (stamps build: 4 x 32 stamps) + the next chunk's GroupNorm affine (2 x 32 f32)
+  constexpr size_t lds = 396 * 64 + 2 * 3 * 128 * 64 + 1024 + 256;
   p.ntn = p.Cout / 128;
   p.epi_nt = g_epi_nt == 2 ? ((long long)p.M * p.out_ld * (long long)sizeof(TO) > (256ll << 20)) : g_epi_nt;
   g_last_epi_nt = p.epi_nt;
