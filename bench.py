@@ -23,6 +23,7 @@ import glob
 import json
 import math
 import os
+import re
 import sys
 import time
 
@@ -339,7 +340,12 @@ def pmc_traffic(kernel_prefix, tag):
     """HBM bytes per launch of the dominant kernel from the committed PMC profile
     (profiles/*_pmc_traffic.json, tools/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950 correction +
     WRITE_SIZE) for this config tag; None when absent."""
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+    def newest_first(path):  # profiles/rNN<suffix>_...: round, then suffix length, then suffix (v < ak)
+        tag = os.path.basename(path).split("_")[0]
+        m = re.match(r"r(\d+)([a-z]*)$", tag)
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, tag)
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=newest_first, reverse=True):
         with open(path) as f:
             d = json.load(f)
         if d.get("kernel", "").startswith(kernel_prefix) and d.get("config", "c2") == tag:
