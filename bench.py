@@ -437,7 +437,7 @@ def run(args):
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     net = ncsnpp.NCSNppHIP(formula_weights(), dtype=dtype, device=dev)
     sde = sampler.SDESpec("ouve", theta=1.5, sigma_min=0.05, sigma_max=0.5)
-    enh = PCEnhancer(net, sde, N=args.N, streams=args.streams)
+    enh = PCEnhancer(net, sde, N=args.N, streams=args.streams, stagger=bool(args.stagger))
     probe_enh = PCEnhancer(net, sde, N=min(args.N, 2))  # kernel durations do not depend on N
     B = args.batch
     y = torch.from_numpy(synth_clips(B, args.seconds, 1000 * rank)).to(dev)
@@ -554,6 +554,8 @@ def main():
     ap.add_argument("--conv-variant", type=int, default=0, help="snrse conv_variant option (0 = auto)")
     ap.add_argument("--streams", type=int, default=1,
                     help="PC-sampler lanes per GPU, each on its own HIP stream (snrse.enhance.PCEnhancer)")
+    ap.add_argument("--stagger", type=int, default=1,
+                    help="with --streams > 1: start each lane half a network evaluation after the previous one")
     ap.add_argument("--cpu-full", default=None, metavar="PATH",
                     help="only run the CPU baseline with one full N=30 utterance and write it to PATH")
     args = ap.parse_args()

@@ -53,16 +53,19 @@ class PCEnhancer:
     streams > 1 splits the batch into that many lanes, each on its own HIP stream with its own
     GroupNorm-statistics arena and split-K workspace, and issues their network evaluations
     alternately (sampler.pc_sample_lockstep): one lane's latency-bound low-resolution levels overlap
-    the other lane's full-resolution GEMMs.  The noise draws are the whole-batch ones (LaneNoise), so
-    the result equals the single-stream run."""
+    the other lane's full-resolution GEMMs.  stagger: lane k starts when lane k-1's first evaluation
+    has reached the middle of the network (an event recorded between its down and up paths), so the
+    lanes run half an evaluation apart instead of in phase.  The noise draws are the whole-batch ones
+    (LaneNoise), so the result equals the single-stream run."""
 
     def __init__(self, net, sde: sampler.SDESpec, N=30, eps=0.03, snr=0.5, predictor="reverse_diffusion",
-                 corrector="ald", corrector_steps=1, score_mode=0, transform="exponent", streams=1):
+                 corrector="ald", corrector_steps=1, score_mode=0, transform="exponent", streams=1, stagger=True):
         self.net, self.sde, self.N, self.eps, self.snr = net, sde, N, eps, snr
         self.mode = transform_mode(transform)
         self.predictor, self.corrector, self.corrector_steps = predictor, corrector, corrector_steps
         self.score_mode = score_mode
         self.streams = int(streams)
+        self.stagger = bool(stagger)
         self._lane_streams = {}
 
     def _iter(self, Y, noise):
@@ -103,7 +106,23 @@ class PCEnhancer:
             with torch.cuda.stream(s):
                 Yh = Y[a:b].contiguous()
                 lanes.append((s, self._iter(Yh, sampler.LaneNoise(noise, a, b, B))))
-        res = sampler.pc_sample_lockstep(lanes)
+        starts = None
+        if self.stagger:
+            # lane k's first launch waits for lane k-1's first evaluation to pass the bottleneck
+            evs = [torch.cuda.Event() for _ in range(nl - 1)]
+
+            def arm(k):
+                if k + 1 < nl:
+                    self.net.mid_hook = lambda: evs[k].record(torch.cuda.current_stream())
+
+            def start(k):
+                if k > 0:
+                    torch.cuda.current_stream().wait_event(evs[k - 1])
+                arm(k)
+
+            starts = start
+        res = sampler.pc_sample_lockstep(lanes, on_first=starts)
+        self.net.mid_hook = None
         for (s, _), (x, _) in zip(lanes, res):
             cur.wait_stream(s)
             x.record_stream(cur)

@@ -122,6 +122,7 @@ class NCSNppHIP:
         self.device = torch.device(device)
         self._arena = None  # ops.StatsArena of the GroupNorm statistics, one fill per evaluation
         self._arenas = {}   # one arena per launch stream (the two-stream sampler runs evaluations concurrently)
+        self.mid_hook = None  # callable run once between the down and the up path of the next evaluation
         check_topology(**cfg)
         self.plan = build_plan(**cfg)
         dev, dt = self.device, dtype
@@ -290,6 +291,9 @@ class NCSNppHIP:
         h = self._resblock(plan[i], h, None, dense); i += 1  # noqa: E702
         h = self._attn(plan[i], h); i += 1  # noqa: E702
         h = self._resblock(plan[i], h, None, dense); i += 1  # noqa: E702
+        if self.mid_hook is not None:  # one-shot callback between the down and the up path (lane stagger)
+            hook, self.mid_hook = self.mid_hook, None
+            hook()
         pyr = None
         for lvl in reversed(range(nres)):
             for _ in range(3):

@@ -157,19 +157,25 @@ def pc_sample(score_step, Y, sde: SDESpec, N=30, eps=0.03, snr=0.5, predictor="r
             return e.value
 
 
-def pc_sample_lockstep(lanes):
+def pc_sample_lockstep(lanes, on_first=None):
     """Run several PC loops (one per half-batch) with their launches interleaved step by step, each
     on its own HIP stream and split-K workspace: `lanes` = [(stream, pc_sample_iter generator)].
     While one lane's network evaluation is in its latency-bound low-resolution levels, the other
-    lane's full-resolution GEMMs fill the chip.  Returns [(x_result, nfe)] in lane order."""
+    lane's full-resolution GEMMs fill the chip.  on_first(k) runs on lane k's stream before its first
+    step (the enhancer's stagger).  Returns [(x_result, nfe)] in lane order."""
     out = [None] * len(lanes)
     live = list(range(len(lanes)))
+    first = [True] * len(lanes)
     while live:
         for k in list(live):
             stream, it = lanes[k]
             dev = stream.device
             with torch.cuda.stream(stream):
                 ops.use_workspace_lane(k, dev)
+                if first[k]:
+                    first[k] = False
+                    if on_first is not None:
+                        on_first(k)
                 try:
                     next(it)
                 except StopIteration as e:
