@@ -113,7 +113,7 @@ int snrse_set_workspace(void* ptr, size_t bytes);
 /* Tuning switches (A/B experiments; the Python host also reads SNRSE_OPTS="name=value,..." at load):
  * "conv_variant" 0 auto, 1 register-staged v1, 2 LDS-DMA v2, 5 halo GEMM v5 (the default halo kernel);
  * "splitk" 0 disables the split-K small-image GEMMs, "splitk_target" workgroups a split launch aims for;
- * "epi_nt" 0 / 1 / 2 (auto above 256 MB of output) non-temporal halo-GEMM output stores;
+ * "epi_nt" 0 / 1 / 2 (auto above "epi_nt_mb" = 256 MB of output) non-temporal halo-GEMM output stores;
  * "h5_specialise" 1 compile-time epilogue flags for the NCSN++ ResBlock configurations;
  * "h5_persist" / "h5_stagger" persistent staggered halo launches (measured slower: off);
  * "resample_variant" 0 row-strip / 1 LDS-tiled gn_resample, "resample_nt" non-temporal stores there,

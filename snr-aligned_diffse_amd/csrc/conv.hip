@@ -1231,6 +1231,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 #endif
 }
 
+int g_epi_nt_mb = 256;                // option "epi_nt_mb": output size (MB) above which epi_nt = 2 streams
 int g_epi_nt = 2;                     // option "epi_nt": non-temporal epilogue stores of the v5 halo GEMM:
                                       // 0 off, 1 on, 2 when the output exceeds the 256 MB Infinity
                                       // Cache (+1 % on the full-resolution convs, tools/h5_sweep.py)
@@ -1260,7 +1261,8 @@ int launch_halo5_gn(ConvParams p, hipStream_t s) {
   // halo + weight ring + (stamps build: 4 x 32 stamps) + the next chunk's GroupNorm affine (2 x 32 f32)
   constexpr size_t lds = 396 * 64 + 2 * 3 * 128 * 64 + 1024 + 256;
   p.ntn = p.Cout / 128;
-  p.epi_nt = g_epi_nt == 2 ? ((long long)p.M * p.out_ld * (long long)sizeof(TO) > (256ll << 20)) : g_epi_nt;
+  p.epi_nt = g_epi_nt == 2 ? ((long long)p.M * p.out_ld * (long long)sizeof(TO) > ((long long)g_epi_nt_mb << 20))
+                           : g_epi_nt;
   g_last_epi_nt = p.epi_nt;
   const int tiles = p.B * (p.H / 4) * (p.W / 64) * p.ntn;
   int grid = tiles;
@@ -1532,6 +1534,7 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   if (name_is(name, "splitk_target")) { *value = g_splitk_target; return 0; }
   if (name_is(name, "h5_persist")) { *value = g_h5_persist; return 0; }
   if (name_is(name, "epi_nt")) { *value = g_epi_nt; return 0; }
+  if (name_is(name, "epi_nt_mb")) { *value = g_epi_nt_mb; return 0; }
   if (name_is(name, "h5_stagger")) { *value = g_h5_stagger_per_phase; return 0; }
   if (name_is(name, "h5_specialise")) { *value = g_h5_specialise; return 0; }
   if (name_is(name, "stats_zeroed")) { *value = g_snrse_stats_zeroed; return 0; }
@@ -1551,6 +1554,7 @@ extern "C" int snrse_set_option(const char* name, int value) {
   if (name_is(name, "splitk_target")) { g_splitk_target = value > 0 ? value : 256; return 0; }
   if (name_is(name, "h5_persist")) { g_h5_persist = value; return 0; }
   if (name_is(name, "epi_nt")) { g_epi_nt = value; return 0; }
+  if (name_is(name, "epi_nt_mb")) { g_epi_nt_mb = value > 0 ? value : 256; return 0; }
   if (name_is(name, "h5_stagger")) { g_h5_stagger_per_phase = value; return 0; }
   if (name_is(name, "h5_specialise")) { g_h5_specialise = value; return 0; }
   if (name_is(name, "stats_zeroed")) { g_snrse_stats_zeroed = value ? 1 : 0; return 0; }
