@@ -151,6 +151,10 @@ __global__ __launch_bounds__(256) void input_pack_kernel(const float2* x, const 
 // LDS, one f64 atomic pair per channel per workgroup (slot = blockIdx & 15).  Also writes the f32 input pyramid.
 // Contract: W % 64 == 0, (H * W / 64) % 16 == 0 (a workgroup's 16 tiles lie in one image).
 constexpr int IC_TPW = 4;  // 64-px tiles per wave
+#ifndef SNRSE_IC_NT
+#define SNRSE_IC_NT 1  // non-temporal stores of the 256-B-per-pixel activation (its 1 GB at C2 exceeds the
+                         // Infinity Cache: 417-432 -> 329-332 us per launch, profiles/r02ay_input_conv_nt_ab.log)
+#endif
 SNRSE_DEV f32x4 mfma_bf16_16x16x32(const u32x4& a, const u32x4& b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, a), __builtin_bit_cast(bf16x8_mfma, b),
                                                  c, 0, 0, 0);
@@ -269,7 +273,8 @@ __global__ __launch_bounds__(256) void input_conv_kernel(const float2* __restric
       const auto r0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
       const auto r1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
       const u32x4 o = {r0[0], r1[0], r0[1], r1[1]};
-      *(u32x4*)(orow + 16 * (2 * jp + (g & 1))) = o;
+      if (SNRSE_IC_NT) __builtin_nontemporal_store(o, (u32x4*)(orow + 16 * (2 * jp + (g & 1))));
+      else *(u32x4*)(orow + 16 * (2 * jp + (g & 1))) = o;
     }
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
