@@ -152,8 +152,9 @@ __global__ __launch_bounds__(256) void input_pack_kernel(const float2* x, const 
 // Contract: W % 64 == 0, (H * W / 64) % 16 == 0 (a workgroup's 16 tiles lie in one image).
 constexpr int IC_TPW = 4;  // 64-px tiles per wave
 #ifndef SNRSE_IC_NT
-#define SNRSE_IC_NT 1  // non-temporal stores of the 256-B-per-pixel activation (its 1 GB at C2 exceeds the
-                         // Infinity Cache: 417-432 -> 329-332 us per launch, profiles/r02ay_input_conv_nt_ab.log)
+#define SNRSE_IC_NT 0  // non-temporal stores of the 256-B-per-pixel activation: faster in an isolated
+                         // micro-bench (420 -> 330 us), slower inside the network (383-388 -> 450 us per launch,
+                         // profiles/r02bd_input_conv_nt_insitu.log): off
 #endif
 SNRSE_DEV f32x4 mfma_bf16_16x16x32(const u32x4& a, const u32x4& b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, a), __builtin_bit_cast(bf16x8_mfma, b),
