@@ -493,6 +493,15 @@ def run(args):
                 "other_conv_kernels": {k: {"launches": v[2], "ms": v[1], "tflops": v[0] / max(v[1], 1e-9) / 1e9}
                                        for k, v in by.items() if k != kname}}
 
+    parity = None
+    if rank == 0 and not args.no_parity:
+        # the timed network object itself on the reference's N=5 OUVE PC run (paritycheck.py), after the
+        # timed region: pins the benched code's numerics in the same JSON line
+        import paritycheck
+        r = paritycheck.pc_vs_golden(dev, net)
+        parity = {k: r[k] for k in ("check", "dtype", "rel_rms", "abs_rms", "golden_rms", "tol_rel", "ok")}
+        parity["golden"] = "tests/golden/pc_ouve.npz"
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         cpu = cpu_baseline()
@@ -523,7 +532,7 @@ def run(args):
             "data": "synthetic (SURVEY §8d harmonic+noise clips; formula weights of the NCSN++ architecture)",
             "config": {"workload": wl, "global_batch": B * world, "per_gpu_batch": B, "seq_len": T_frames,
                        "parallelism": f"dp{world} (utterance sharding)"},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "cpu_baseline": cpu, "parity": parity,
             "output_rms_mean": float(allm.mean()),
         }
         if sdist.oversubscribed(world):  # a launcher rehearsal: ranks share the visible GPU(s)
@@ -551,6 +560,8 @@ def main():
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the post-run parity check of the benched network vs tests/golden/pc_ouve.npz")
     ap.add_argument("--conv-variant", type=int, default=0, help="snrse conv_variant option (0 = auto)")
     ap.add_argument("--streams", type=int, default=1,
                     help="PC-sampler lanes per GPU, each on its own HIP stream (snrse.enhance.PCEnhancer)")

@@ -115,7 +115,6 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  * "splitk" 0 disables the split-K small-image GEMMs, "splitk_target" workgroups a split launch aims for;
  * "epi_nt" 0 / 1 / 2 (auto above "epi_nt_mb" = 256 MB of output) non-temporal halo-GEMM output stores;
  * "h5_specialise" 1 compile-time epilogue flags for the NCSN++ ResBlock configurations;
- * "h5_persist" / "h5_stagger" persistent staggered halo launches (measured slower: off);
  * "resample_variant" 0 row-strip / 1 LDS-tiled gn_resample, "resample_nt" non-temporal stores there,
  * "resample_down_rows" 1 / 2 (default) / 4 output rows per down-sampling row strip (bit-identical results);
  * "stats_zeroed" 1 = the statistics buffers handed to snrse_conv2d / snrse_gn_stats are already zero (the

@@ -1,0 +1,140 @@
+"""Parity checks of the exact benched bf16 path, shared by `__graft_entry__.smoke()` and bench.py.
+
+TEST INFRASTRUCTURE (like tests/): it reads the committed reference-generated fixtures under
+tests/golden/ and fp32 torch references; nothing on the product path imports it.  Each check runs the
+product kernels through the C-ABI (snrse.ops / snrse.ncsnpp) and returns a small dict of errors with the
+tolerance it is held to, so a driver-run record (smoke log, bench JSON line) carries the numbers.
+
+* `bf16_nfe_vs_golden`: one bf16 NCSNppHIP evaluation at [2, 2, 256, 64] against the reference module's
+  fp32 output (tests/golden/ncsnpp_full.npz, tools/gen_golden.py; reference ncsnpp.py:247-404).
+* `halo_level0_vs_fp32`: one full-size C2 level-0 Conv_0 launch of the dominant kernel
+  (conv_halo5_kernel: B=32, 256 x 512, 128 -> 128, GroupNorm+SiLU prologue, temb, statistics,
+  non-temporal epilogue) against fp32 F.conv2d of the same bf16 operands on three images
+  (reference layerspp.py:244-266).
+* `pc_vs_golden`: the PC loop exactly as bench.py times it (snrse.enhance.PCEnhancer on the given net)
+  for the reference's own N = 5 OUVE run (tests/golden/pc_ouve.npz; sampling/__init__.py:54-75,
+  predictors.py:75-80, correctors.py:69-81) with the recorded noise draws.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "snr-aligned_diffse_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+# bf16 tolerances (relative RMS on the complex spectrogram): a single bf16 NFE and the N = 5 loop are
+# held to 2e-2 (tests/test_gpu_kernels.py test_ncsnpp_full_golden, tests/test_gpu_c2_path.py
+# BF16_PC_TOL); the fp32 parity mode to 1e-4 (the north star's bound).  One halo launch vs fp32 conv of
+# the same bf16 operands: 1e-2 (test_halo_c2_level0_nontemporal).
+TOL = {"nfe": {"bf16": 2e-2, "fp32": 1e-4}, "pc": {"bf16": 2e-2, "fp32": 1e-4}, "halo": 1e-2}
+
+
+def _golden(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def _rel(a, b):
+    a = torch.as_tensor(a).detach().cpu().to(torch.complex128 if torch.as_tensor(a).is_complex() else torch.float64)
+    b = torch.as_tensor(b).detach().cpu().to(a.dtype)
+    return float((a - b).abs().pow(2).mean().sqrt() / (b.abs().pow(2).mean().sqrt() + 1e-30))
+
+
+def _abs_rms(a, b):
+    a = torch.as_tensor(a).detach().cpu().to(torch.complex128 if torch.as_tensor(a).is_complex() else torch.float64)
+    b = torch.as_tensor(b).detach().cpu().to(a.dtype)
+    return float((a - b).abs().pow(2).mean().sqrt())
+
+
+def formula_weights():
+    from snrse import formula
+    with open(os.path.join(GOLDEN, "state_dict_keys.json")) as f:
+        shapes = {k: tuple(s) for k, s in json.load(f)["ncsnpp"]}
+    return {k: torch.from_numpy(v) for k, v in formula.formula_state_dict(shapes).items()}
+
+
+def _dtname(dtype):
+    return "bf16" if dtype == torch.bfloat16 else "fp32"
+
+
+def bf16_nfe_vs_golden(dev, net=None, dtype=torch.bfloat16):
+    from snrse import formula, ncsnpp
+    g = _golden("ncsnpp_full.npz")
+    net = net or ncsnpp.NCSNppHIP(formula_weights(), dtype=dtype, device=dev)
+    x = torch.from_numpy(formula.normal_tensor("golden.ncsnpp.x", (2, 2, 256, 64), True)) * 0.5
+    t = torch.tensor([0.5, 0.8], device=dev)
+    out = net.dnn(x[:, 0].contiguous().to(dev), x[:, 1].contiguous().to(dev), t)
+    torch.cuda.synchronize(dev)
+    d = _dtname(net.dtype)
+    r = {"check": "one NCSN++ NFE [2,2,256,64] vs reference golden ncsnpp_full.npz", "dtype": d,
+         "rel_rms": _rel(out, g["out"][:, 0]), "abs_rms": _abs_rms(out, g["out"][:, 0]), "tol_rel": TOL["nfe"][d]}
+    r["ok"] = bool(np.isfinite(r["rel_rms"]) and r["rel_rms"] < r["tol_rel"])
+    return r
+
+
+def halo_level0_vs_fp32(dev, images=(0, 17, 31), seed=11):
+    """One C2 level-0 Conv_0 launch (B=32, 256x512, 128->128) through snrse_conv2d, vs fp32 torch."""
+    import torch.nn.functional as F
+    from snrse import ops
+    B, H, W, C = 32, 256, 512, 128
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = (torch.randn(B, H, W, C, device=dev, generator=g) * 1.3 + 0.1).bfloat16()
+    w = (torch.randn(C, 3, 3, C, device=dev, generator=g) / math.sqrt(9 * C)).bfloat16()
+    bias = torch.randn(C, device=dev, generator=g) * 0.1
+    gam = torch.rand(C, device=dev, generator=g) + 0.5
+    bet = torch.randn(C, device=dev, generator=g) * 0.2
+    temb = torch.randn(B, C + 40, device=dev, generator=g)
+    sums, _ = ops.gn_stats(x)
+    gn = ops.gn_scale_shift(sums, gam, bet, H * W)
+    st = ops.new_stats(B, C)
+    out = ops.conv2d(x, w.reshape(C, -1).contiguous(), 3, C, bias=bias, stats=st, gn=gn, temb=temb, temb_off=40)
+    kern = ops.kernel_name(ops.get_option("last_kernel"))
+    nt = ops.get_option("last_epi_nt")
+    torch.cuda.synchronize(dev)
+    folded = ops.fold_stats(st)
+    errs, serrs = [], []
+    for b in images:
+        xb = x[b].float().permute(2, 0, 1)[None]
+        a = F.silu(xb * gn[0][b][None, :, None, None] + gn[1][b][None, :, None, None]).bfloat16().float()
+        ref = F.conv2d(a, w.float().permute(0, 3, 1, 2), bias, padding=1)[0] + temb[b, 40:40 + C, None, None]
+        errs.append(_rel(out[b].float().permute(2, 0, 1), ref))
+        o = out[b].double()
+        serrs.append(_rel(folded[b], torch.stack([o.sum((0, 1)), (o * o).sum((0, 1))], -1)))
+    del x, out
+    r = {"check": "full-size C2 level-0 Conv_0 launch (B=32, 256x512, 128->128, GN+SiLU+temb+stats) vs fp32 conv",
+         "kernel": kern, "nontemporal_epilogue": bool(nt), "images": list(images), "rel_rms": max(errs),
+         "stats_rel": max(serrs), "tol_rel": TOL["halo"]}
+    r["ok"] = bool(kern == "conv_halo5_kernel" and np.isfinite(r["rel_rms"]) and r["rel_rms"] < r["tol_rel"]
+                   and r["stats_rel"] < 3e-3)
+    return r
+
+
+def pc_vs_golden(dev, net=None, dtype=torch.bfloat16):
+    """PCEnhancer.sample (bench.py's class) on the reference's N = 5 OUVE run with its noise draws."""
+    from snrse import formula, ncsnpp, sampler
+    from snrse.enhance import PCEnhancer
+    g = _golden("pc_ouve.npz")
+    net = net or ncsnpp.NCSNppHIP(formula_weights(), dtype=dtype, device=dev)
+    Y = (torch.from_numpy(formula.normal_tensor("golden.pc.Y", (2, 1, 256, 64), True)) * 0.5)[:, 0].contiguous().to(dev)
+    enh = PCEnhancer(net, sampler.SDESpec("ouve", theta=1.5, sigma_min=0.05, sigma_max=0.5), N=5)
+
+    def tape(i):
+        return torch.from_numpy(formula.normal_tensor(f"golden.pc.noise.{i}", (2, 1, 256, 64), True)).to(dev)[:, 0]
+
+    x, nfe = enh.sample(Y, sampler.NoiseSource(tape=tape))
+    torch.cuda.synchronize(dev)
+    d = _dtname(net.dtype)
+    r = {"check": "PCEnhancer N=5 OUVE (reverse_diffusion + ald, 10 NFE) [2,256,64] vs reference golden pc_ouve.npz",
+         "dtype": d, "nfe": nfe, "rel_rms": _rel(x, g["out"][:, 0]), "abs_rms": _abs_rms(x, g["out"][:, 0]),
+         "golden_rms": float(np.sqrt(np.mean(np.abs(g["out"]) ** 2))), "tol_rel": TOL["pc"][d]}
+    r["ok"] = bool(nfe == 10 and np.isfinite(r["rel_rms"]) and r["rel_rms"] < r["tol_rel"])
+    return r

@@ -840,133 +840,17 @@ __global__ __launch_bounds__(256) void conv_splitk_finalize(ConvParams p, int pp
 // prologue / epilogue runs under the other's MFMAs (v4 is 1 workgroup/CU, 152 KB).
 SNRSE_DEV int swz64(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >> 1) & 3)) << 4); }
 
-#ifndef SNRSE_H5_PRIO
-#define SNRSE_H5_PRIO 0  // measured 1-2 % slower with the priority bump (tools/conv_bench.py A/B): off
+#ifndef SNRSE_H5_OPAQUE
+#define SNRSE_H5_OPAQUE 0
 #endif
-constexpr bool g_h5_prio_dev = SNRSE_H5_PRIO;  // s_setprio around the MFMA block of each tap
 SNRSE_DEV int h5_opaque(int v) {
   int r;
   asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
   return r;
 }
 
-// per-CU arrival counter of the persistent v5 launches (key = XCC << 8 | HW_ID[15:8]); exactly two
-// workgroups per CU per launch keep each count's parity = arrival order
-__device__ unsigned g_h5_cu_arrivals[8 * 256];
-
-#ifndef SNRSE_H5_SWAP
-#define SNRSE_H5_SWAP 0  // swapped operands + register epilogue: correct but 3 % slower (scattered 16-B stores; A/B ABA 12.05/12.03 vs 12.41 utt/s): off
-#endif
-template <int CTRL>
-SNRSE_DEV float h5_dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
-}
-// sum over the 16 lanes of a DPP row (every lane of the row receives it)
-SNRSE_DEV float h5_row_sum16(float v) {
-  v += h5_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += h5_dpp<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += h5_dpp<0x141>(v);  // row_half_mirror
-  v += h5_dpp<0x140>(v);  // row_mirror
-  return v;
-}
-
-// v5 epilogue with swapped MFMA operands (D = [co][px], lane (g = lane >> 4, lr = lane & 15) of
-// block (h, i, j) holds channels n0 + 64h + 16j + 4g + e of pixel 16i + lr): the accumulators of
-// channel blocks (2jp, 2jp + 1) are exchanged between DPP rows (v_permlane16_swap), so every lane
-// owns 8 consecutive channels of one pixel -- bias / temb / residual / Combine and the 16-byte
-// store straight from registers, no LDS staging.  GroupNorm statistics: per-lane sums over the 4
-// pixel blocks, DPP row sums over the 16 pixels, one LDS row per wave for block_stats_flush.
-template <typename TO>
-SNRSE_DEV void epilogue_swapped(const ConvParams& p, const f32x4 (&acc)[2][4][4], int mrow, int n0, int lane,
-                                float* red, int wid, int b) {
-  const int g = lane >> 4, lr = lane & 15;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int jp = 0; jp < 2; ++jp) {
-      const int nl = 64 * h + 16 * (2 * jp + (g & 1)) + 8 * (g >> 1);  // channel offset within the tile
-      const int n = n0 + nl;
-      float add[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) add[k] = 0.f;
-      if (p.bias) {
-        const f32x4 b0 = *(const f32x4*)(p.bias + n), b1 = *(const f32x4*)(p.bias + n + 4);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) { add[k] += b0[k]; add[k + 4] += b1[k]; }
-      }
-      if (p.temb) {
-        const float* tb = p.temb + (size_t)b * p.temb_stride + n;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) add[k] += tb[k];
-      }
-      u32x4 rv[4];
-      f32x4 qv[4];
-      if (p.res) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) rv[i] = *(const u32x4*)((const TO*)p.res + ((size_t)mrow + 16 * i + lr) * p.res_ld + n);
-      }
-      if (p.comb_src) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) qv[i] = *(const f32x4*)(p.comb_src + ((size_t)mrow + 16 * i + lr) * 4);
-      }
-      float s1[8], s2[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        f32x4 a = acc[h][i][2 * jp], bq = acc[h][i][2 * jp + 1];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[e]), __float_as_uint(bq[e]), false, false);
-          a[e] = __uint_as_float(r[0]);
-          bq[e] = __uint_as_float(r[1]);
-        }
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { v[e] = a[e] + add[e]; v[e + 4] = bq[e] + add[e + 4]; }
-        if (p.res) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            v[2 * k] += __uint_as_float(rv[i][k] << 16);
-            v[2 * k + 1] += __uint_as_float(rv[i][k] & 0xffff0000u);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] *= p.out_scale;
-        if (p.comb_src) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const f32x4 w = *(const f32x4*)(p.comb_w + (size_t)(n + k) * 4);
-            v[k] += qv[i][0] * w[0] + qv[i][1] * w[1] + qv[i][2] * w[2] + qv[i][3] * w[3] + p.comb_b[n + k];
-          }
-        }
-        const u32x4 o = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
-                         pack_bf16x2(v[6], v[7])};
-        TO* dst = (TO*)p.out + ((size_t)mrow + 16 * i + lr) * p.out_ld + n;
-        if (p.epi_nt) __builtin_nontemporal_store(o, (u32x4*)dst);
-        else *(u32x4*)dst = o;
-        if (p.stats) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) { s1[k] += v[k]; s2[k] = fmaf(v[k], v[k], s2[k]); }
-        }
-      }
-      if (p.stats) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float a1 = h5_row_sum16(s1[k]), a2 = h5_row_sum16(s2[k]);
-          if (lr == 0) {
-            red[(wid * 128 + nl + k) * 2] = a1;
-            red[(wid * 128 + nl + k) * 2 + 1] = a2;
-          }
-        }
-      }
-    }
-  }
-}
-
 template <typename TO, int GNM, int EF>
 __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
-  constexpr bool H5SW = SNRSE_H5_SWAP && sizeof(TO) == 2;  // swapped operands + register epilogue
   constexpr int TH = 4, TW = 64, HC = TW + 2;
   constexpr int HROWS = (TH + 2) * HC;  // 396
   constexpr int HJ = 7;                 // halo rows per thread: (tid >> 2) + 64 j
@@ -983,7 +867,13 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   // thread keeps them in registers across the MFMA phases
   float* const gnl = (float*)(smem + HALO_BYTES + 2 * SLOT + 1024);  // past the stamps build's area
 
+#if SNRSE_H5_OPAQUE
+  // lane-derived values come from an opaque copy of the thread index, so the compiler re-derives
+  // them where they are used instead of keeping them in VGPRs across the whole kernel
+  const int tid = h5_opaque((int)threadIdx.x), lane = tid & 63;
+#else
   const int tid = threadIdx.x, lane = tid & 63;
+#endif
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
 #ifdef SNRSE_STAMPS
   unsigned long long* const lst = (unsigned long long*)(ring + 2 * SLOT) + wid * 32;
@@ -992,36 +882,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   const int nb = gridDim.x, bid = blockIdx.x;
   const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7, pos = bid >> 3;
   const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
-  // persistent mode: workgroup g runs the contiguous tile range [t_begin, t_end) (consecutive g
-  // share an XCD, so an XCD walks neighbouring image rows).  The second workgroup to arrive on a
-  // CU starts p.h5_stagger ticks late, so the two co-resident workgroups' prologues / epilogues
-  // (HBM-latency and store bound) run under the other's MFMAs instead of in lockstep.
-  int t_begin = g, t_end = g + 1;
-  if (p.h5_tiles > 0) {
-    t_begin = (int)((long long)g * p.h5_tiles / nb);
-    t_end = (int)((long long)(g + 1) * p.h5_tiles / nb);
-    if (p.h5_stagger > 0) {
-      __shared__ unsigned h5_late;
-      if (tid == 0) {
-        unsigned hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        const unsigned key = ((xcc & 7u) << 8) | ((hw >> 8) & 0xffu);
-        h5_late = atomicAdd(&g_h5_cu_arrivals[key], 1u) & 1u;
-      }
-      __syncthreads();
-      if (h5_late) {
-        const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-        while (__builtin_amdgcn_s_memtime() - t_start < (unsigned long long)p.h5_stagger) __builtin_amdgcn_s_sleep(16);
-      }
-    }
-  }
-  for (int wg = t_begin; wg < t_end; ++wg) {
-  if (wg != t_begin) __syncthreads();  // LDS: the previous tile's epilogue staging is done
-  // lane-derived values are re-derived per tile from an opaque copy of the thread index, so the
-  // tile loop does not hoist them into VGPRs live across the whole tile (256-VGPR budget)
-  const int tid = h5_opaque((int)threadIdx.x), lane = tid & 63;
-  (void)lane;
+  const int wg = g;
   const int n0 = (wg % p.ntn) * 128;
   int tile = wg / p.ntn;
   const int ntw = p.W / TW, nth = p.H / TH;
@@ -1172,17 +1033,13 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
       for (int i = 0; i < 4; ++i) af[i] = *(const u32x4*)(halo + swz64(hbase + i * 16, lg));
 #pragma unroll
       for (int j = 0; j < 8; ++j) bfr[j] = *(const u32x4*)(sb + swz64(j * 16 + lrow, lg));
-      if (g_h5_prio_dev) __builtin_amdgcn_s_setprio(1);  // favour the MFMA stream over the co-resident
-                                                        // workgroup's transform / epilogue waves
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            acc[h][i][j] = H5SW ? mfma_chunk<bf16_t>(bfr[h * 4 + j], af[i], acc[h][i][j])   // D[co][px]
-                                : mfma_chunk<bf16_t>(af[i], bfr[h * 4 + j], acc[h][i][j]);  // D[px][co]
-      if (g_h5_prio_dev) __builtin_amdgcn_s_setprio(0);
+            acc[h][i][j] = mfma_chunk<bf16_t>(af[i], bfr[h * 4 + j], acc[h][i][j]);  // D[px][co]
     }
     SNRSE_STAMP(3 + 2 * (q & 15));
     if (last && c + 1 < ncb) {
@@ -1198,18 +1055,13 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   float* const stage = (float*)(smem + wid * (64 * 68 * 4));
   float* const red = (float*)(smem + 4 * (64 * 68 * 4));
   const int mrow = (bb * p.H + h0 + wid) * p.W + w0;
-  if constexpr (H5SW) {
-    epilogue_swapped<TO>(p, acc, mrow, n0, lane, red, wid, bb);
-  } else {
-    epilogue_img<TO, 4, 128, true, EF>(p, acc[0], mrow, n0, lane, stage, red, wid, bb, n0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    SNRSE_STAMP(26);
-    epilogue_img<TO, 4, 128, true, EF>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0);
-  }
+  epilogue_img<TO, 4, 128, true, EF>(p, acc[0], mrow, n0, lane, stage, red, wid, bb, n0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  SNRSE_STAMP(26);
+  epilogue_img<TO, 4, 128, true, EF>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0);
   SNRSE_STAMP(27);
   if (EF < 0 ? p.stats != nullptr : (EF & EF_STATS) != 0) block_stats_flush<4, 128>(p, red, bb, n0);
-  }  // tile loop
 #ifdef SNRSE_STAMPS
   {
     unsigned long long st_[29];
@@ -1234,13 +1086,9 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 int g_epi_nt_mb = 256;                // option "epi_nt_mb": output size (MB) above which epi_nt = 2 streams
 int g_epi_nt = 2;                     // option "epi_nt": non-temporal epilogue stores of the v5 halo GEMM:
                                       // 0 off, 1 on, 2 when the output exceeds the 256 MB Infinity
-                                      // Cache (+1 % on the full-resolution convs, tools/h5_sweep.py)
+                                      // Cache (+1 % on the full-resolution convs)
 int g_last_epi_nt = 0;                // option read-back "last_epi_nt": store flavour of the latest v5 launch
 int g_last_chunks = 1;                // option read-back "last_chunks": launches of the latest snrse_conv2d
-int g_h5_persist = 0;                 // option "h5_persist": persistent staggered v5 launches (measured
-                                      // 5-10 % slower than one tile per workgroup: off)
-int g_h5_slots = 512;                 // two workgroups per CU (256 CUs)
-int g_h5_stagger_per_phase = 3600;    // option "h5_stagger": s_memtime ticks per phase x nq / 2
 int g_h5_specialise = 1;              // option "h5_specialise": compile-time epilogue flags for the common
                                       // bf16 configurations (0: the run-time flags everywhere)
 
@@ -1265,16 +1113,7 @@ int launch_halo5_gn(ConvParams p, hipStream_t s) {
                            : g_epi_nt;
   g_last_epi_nt = p.epi_nt;
   const int tiles = p.B * (p.H / 4) * (p.W / 64) * p.ntn;
-  int grid = tiles;
-  p.h5_tiles = 0;
-  p.h5_stagger = 0;
-  if (g_h5_persist && tiles >= 4 * g_h5_slots) {  // >= 4 tiles per workgroup: stagger pays off
-    grid = g_h5_slots;
-    p.h5_tiles = tiles;
-    // ~half a tile: a 32-channel chunk of the 9-tap main loop takes ~1.7e3 ticks per phase
-    const int nq = 3 * ((p.C0 + p.C1) / 32) + (p.sc_src ? (p.Csc + p.Csc1) / 32 : 0);
-    p.h5_stagger = g_h5_stagger_per_phase * nq / 2;
-  }
+  const int grid = tiles;
   // the bf16 ResBlock configurations of the NCSN++ path get a branch-free epilogue (bias always on):
   // Conv_0 (+temb), Conv_1 (+residual | +1x1 shortcut as extra K | +Combine), each +-stats, +-NT
   if constexpr (sizeof(TO) == 2 && GNM != 1) {
@@ -1532,10 +1371,8 @@ extern "C" int snrse_get_option(const char* name, int* value) {
   if (name_is(name, "last_kernel")) { *value = g_last_kernel; return 0; }
   if (name_is(name, "splitk")) { *value = g_splitk; return 0; }
   if (name_is(name, "splitk_target")) { *value = g_splitk_target; return 0; }
-  if (name_is(name, "h5_persist")) { *value = g_h5_persist; return 0; }
   if (name_is(name, "epi_nt")) { *value = g_epi_nt; return 0; }
   if (name_is(name, "epi_nt_mb")) { *value = g_epi_nt_mb; return 0; }
-  if (name_is(name, "h5_stagger")) { *value = g_h5_stagger_per_phase; return 0; }
   if (name_is(name, "h5_specialise")) { *value = g_h5_specialise; return 0; }
   if (name_is(name, "stats_zeroed")) { *value = g_snrse_stats_zeroed; return 0; }
   if (name_is(name, "last_ksplit")) { *value = g_last_ksplit; return 0; }
@@ -1552,10 +1389,8 @@ extern "C" int snrse_set_option(const char* name, int value) {
   if (name_is(name, "conv_variant")) { g_conv_variant = value; return 0; }
   if (name_is(name, "splitk")) { g_splitk = value; return 0; }
   if (name_is(name, "splitk_target")) { g_splitk_target = value > 0 ? value : 256; return 0; }
-  if (name_is(name, "h5_persist")) { g_h5_persist = value; return 0; }
   if (name_is(name, "epi_nt")) { g_epi_nt = value; return 0; }
   if (name_is(name, "epi_nt_mb")) { g_epi_nt_mb = value > 0 ? value : 256; return 0; }
-  if (name_is(name, "h5_stagger")) { g_h5_stagger_per_phase = value; return 0; }
   if (name_is(name, "h5_specialise")) { g_h5_specialise = value; return 0; }
   if (name_is(name, "stats_zeroed")) { g_snrse_stats_zeroed = value ? 1 : 0; return 0; }
   if (name_is(name, "resample_variant")) { g_resample_variant = value; return 0; }

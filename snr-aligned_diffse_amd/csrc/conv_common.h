@@ -42,8 +42,6 @@ struct ConvParams {
   float* ws;              // split-K partial sums [ksplit][M][Cout] f32 (caller-registered workspace)
   int ksplit;             // K splits of the v2 GEMM (1: the epilogue runs in the GEMM itself)
   unsigned long long* stamps;  // timing-diagnostic build only (-DSNRSE_STAMPS): [blocks][8][32]
-  int h5_tiles;    // v5 persistent mode: total output tiles (0 = one tile per workgroup)
-  int h5_stagger;  // v5: s_memtime ticks the second workgroup of a CU waits before its first tile
   int epi_nt;      // image-tile epilogue: non-temporal output stores
 };
 
@@ -100,8 +98,47 @@ bool head_ok(const ConvParams& p);
 // 2 = affine + SiLU; `ok` = inside the image (else the conv's zero padding).  Written stage by stage
 // over the 8 elements (8 independent exp / rcp chains) so the schedule can hide the transcendental
 // latencies; element by element the chain was fully serial with an s_nop after every exp and rcp.
+#ifndef SNRSE_XF_PACKED
+#define SNRSE_XF_PACKED 0
+#endif
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
 template <int GNM>
 SNRSE_DEV u32x4 gn_xform8(const u32x4 v, const float* sc, const float* sh, bool ok) {
+#if SNRSE_XF_PACKED
+  // packed-f32 form: the affine, the exp argument, 1 + e and the product run as v_pk_fma / v_pk_mul /
+  // v_pk_add on element pairs (one wave-instruction per 2 elements)
+  f32x2 y[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 xv = {__uint_as_float(v[i] << 16), __uint_as_float(v[i] & 0xffff0000u)};
+    const f32x2 s = {sc[2 * i], sc[2 * i + 1]}, t = {sh[2 * i], sh[2 * i + 1]};
+    y[i] = __builtin_elementwise_fma(xv, s, t);
+  }
+  if constexpr (GNM == 2) {
+    f32x2 e[4];
+    const f32x2 nl2e = {-1.44269504088896341f, -1.44269504088896341f}, one = {1.0f, 1.0f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x2 z = y[i] * nl2e;
+      e[i] = f32x2{__builtin_amdgcn_exp2f(z[0]), __builtin_amdgcn_exp2f(z[1])};
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x2 d = e[i] + one;
+      e[i] = f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) y[i] = y[i] * e[i];
+  }
+  const uint32_t okm = 0u - (uint32_t)ok;
+  u32x4 o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = pack_bf16x2(y[i][0], y[i][1]) & okm;
+  return o;
+#else
   float y[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -127,6 +164,7 @@ SNRSE_DEV u32x4 gn_xform8(const u32x4 v, const float* sc, const float* sh, bool 
 #pragma unroll
   for (int i = 0; i < 4; ++i) o[i] = pack_bf16x2(y[2 * i], y[2 * i + 1]) & okm;
   return o;
+#endif
 }
 
 }  // namespace snrse_conv

@@ -26,12 +26,12 @@ FILE_FLAGS = {name: ["-fno-slp-vectorize"] for name in ("conv.hip", "conv_head.h
                                                           "train.hip")}
 
 
-def _sources():
-    return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+def _sources(csrc=CSRC):
+    return sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")))
 
 
-def _headers():
-    return glob.glob(os.path.join(CSRC, "*.h"))
+def _headers(csrc=CSRC):
+    return glob.glob(os.path.join(csrc, "*.h"))
 
 
 def needs_build() -> bool:
@@ -49,16 +49,17 @@ def _compile(src: str, obj: str, extra=()):
     return obj
 
 
-def build_library(force: bool = False, jobs: int = 8, extra_flags=(), lib: str = LIB) -> str:
+def build_library(force: bool = False, jobs: int = 8, extra_flags=(), lib: str = LIB, csrc: str = CSRC) -> str:
     """Build `lib`.  `extra_flags` (e.g. -DSNRSE_STAMPS for the timing-diagnostic build) go to
-    every compile; such builds use their own object directory next to `lib`."""
+    every compile; such builds use their own object directory next to `lib`.  `csrc` selects another
+    source tree (A/B builds of an earlier revision, tools/build_variant.py)."""
     if lib == LIB and not force and not needs_build():
         return LIB
     objdir = os.path.join(os.path.dirname(lib), "obj")
     os.makedirs(objdir, exist_ok=True)
-    hdr_t = max([os.path.getmtime(h) for h in _headers() + [os.path.abspath(__file__)]] + [0.0])
+    hdr_t = max([os.path.getmtime(h) for h in _headers(csrc) + [os.path.abspath(__file__)]] + [0.0])
     todo, objs = [], []
-    for src in _sources():
+    for src in _sources(csrc):
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_t):
