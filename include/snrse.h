@@ -5,7 +5,13 @@
  * Conventions
  *   - Plain pointers to DEVICE memory, sizes as int, a hipStream_t (NULL = legacy stream);
  *     every launch is stream-ordered and asynchronous, nothing is allocated inside except
- *     where a caller-provided workspace is named.  Entries are reentrant per stream.
+ *     where a caller-provided workspace is named.
+ *   - Reentrancy: entries without a snrse_ctx argument keep no state.  The four with one
+ *     (snrse_conv2d, snrse_gn_stats, snrse_input_conv, snrse_gn_resample) read their switches and
+ *     split-K workspace from it and write their read-backs into it, so calls through DISTINCT
+ *     contexts may run concurrently from any host threads / streams; give each concurrently issuing
+ *     thread or stream its own context.  A NULL context is the process default one (edited by
+ *     snrse_set_option / snrse_set_workspace; for single-stream callers).
  *   - Return 0 on success or a hipError_t code (hipErrorInvalidValue = 1 for a bad
  *     argument); snrse_error_string() maps it to text.  The Python host maps non-zero to
  *     RuntimeError, as the reference's TORCH_CHECK does (op/upfirdn2d.cpp:8-19).
@@ -28,9 +34,19 @@ typedef struct ihipStream_t* hipStream_t;
 
 enum { SNRSE_F32 = 0, SNRSE_BF16 = 1, SNRSE_F16 = 2, SNRSE_F64 = 3 };
 
-int snrse_abi_version(void);
+int snrse_abi_version(void); /* 2: snrse_ctx arguments */
 const char* snrse_error_string(int code);
 int snrse_device_name(char* buf, int len);
+
+/* Caller-owned launch context: tuning switches (the names of snrse_set_option), the split-K
+ * workspace and the read-backs of the latest launch through it (the names of snrse_get_option).
+ * Host memory only; create copies the process default's switches, with no workspace. */
+typedef struct snrse_ctx snrse_ctx;
+snrse_ctx* snrse_ctx_create(void);
+void snrse_ctx_destroy(snrse_ctx* ctx);
+int snrse_ctx_set_workspace(snrse_ctx* ctx, void* ptr, size_t bytes);
+int snrse_ctx_set_option(snrse_ctx* ctx, const char* name, int value);
+int snrse_ctx_get_option(const snrse_ctx* ctx, const char* name, int* value);
 
 /* Generic FIR resampling on [major, in_h, in_w, minor] — replaces the reference's only
  * native op binding, upfirdn2d(input, kernel, up_x, up_y, down_x, down_y, pad_x0, pad_x1,
@@ -55,13 +71,13 @@ int snrse_upfirdn2d(const void* in, void* out, const float* kernel, int major, i
  *   out_f32: write float output (bf16 mode pyramid heads); res then is float too.
  *   stats (optional): per-channel (sum, sumsq) of out, [B][SNRSE_STAT_SLOTS][Cout][2] double
  *          (atomics spread over the slots; consumers fold them), for the next GroupNorm
- *          (zeroed by the call).
+ *          (zeroed by the call unless the context's "stats_zeroed" switch is set).
  *   gn_scale/gn_shift (optional, [B][C0+C1] f32, from snrse_gn_scale_shift): the main input
  *          is consumed as SiLU(x*scale+shift) (gn_act=1) or x*scale+shift (gn_act=0), i.e. the
  *          ResBlock's GroupNorm+SiLU fused into the GEMM's halo load (bf16, 3x3, H%4==0,
  *          W%64==0, and the pyramid heads Cout<=16 with f32 output; otherwise
  *          hipErrorInvalidValue). */
-int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, int B, int H, int W, int ksize,
+int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void* src1, int C1, int B, int H, int W, int ksize,
                  const void* wgt, const void* sc_src, int Csc, const void* sc_src1, int Csc1,
                  const void* sc_wgt, const float* bias, const float* temb, int temb_stride,
                  const void* res, int res_ld, float out_scale, const float* comb_src,
@@ -74,7 +90,7 @@ int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, int B, int 
 
 /* GroupNorm statistics (nn.GroupNorm, layerspp.py:221,233): per-channel (sum, sumsq) over
  * H*W of src0 into sums and of src1 into sums1 (slotted layout above; zeroed by the call). */
-int snrse_gn_stats(const void* src0, int C0, const void* src1, int C1, int B, int HW, double* sums,
+int snrse_gn_stats(snrse_ctx* ctx, const void* src0, int C0, const void* src1, int C1, int B, int HW, double* sums,
                    double* sums1, int dtype, hipStream_t stream);
 
 /* Per-(b, c) GroupNorm scale/shift from per-channel sums (of src0 | src1, H*W pixels each). */
@@ -94,7 +110,7 @@ int snrse_gn_apply(const void* src0, int C0, const void* src1, int C1, int B, in
  * layerspp.py:249/255), both [B][Ho][Wo][C] from one pass over x.  scale/shift [B][C] f32 from
  * snrse_gn_scale_shift, or both NULL (identity).  mode 1 down (H, W even), 2 up.  C % 8 == 0 with C / 8
  * dividing 64 (the row-strip kernel), otherwise C % 16 == 0 (the LDS-tiled kernel). */
-int snrse_gn_resample(const void* src, int C, int B, int H, int W, const float* scale, const float* shift,
+int snrse_gn_resample(snrse_ctx* ctx, const void* src, int C, int B, int H, int W, const float* scale, const float* shift,
                       int act, int mode, void* out_act, void* out_raw, hipStream_t stream);
 
 /* Elementwise GroupNorm-apply (+SiLU) of the channel concatenation (src0 | src1), bf16, from
@@ -102,15 +118,15 @@ int snrse_gn_resample(const void* src, int C, int B, int H, int W, const float* 
 int snrse_gn_act(const void* src0, int C0, const void* src1, int C1, int B, int HW, const float* scale,
                  const float* shift, int act, void* out, hipStream_t stream);
 
-/* Split-K workspace of the small-image conv GEMMs (levels whose tile grid underfills the CUs): a
- * device buffer of `bytes` the caller keeps alive and leaves untouched while convs run; the library
- * keeps [splits][M][Cout] f32 partial sums there and splits only when they fit.  NULL disables
- * splitting (the default).  The pointer is captured when a conv is launched: launches that may run
- * concurrently (different streams) must be issued behind different workspaces (snrse.ops
- * use_workspace_lane does this for the two-stream sampler). */
+/* Split-K workspace of the small-image conv GEMMs (levels whose tile grid underfills the CUs) of the
+ * process default context (per context: snrse_ctx_set_workspace): a device buffer of `bytes` the
+ * caller keeps alive and leaves untouched while convs run; the library keeps [splits][M][Cout] f32
+ * partial sums there and splits only when they fit.  NULL disables splitting (the default).  Launches
+ * that may run concurrently must be issued through contexts with different workspaces. */
 int snrse_set_workspace(void* ptr, size_t bytes);
 
-/* Tuning switches (A/B experiments; the Python host also reads SNRSE_OPTS="name=value,..." at load):
+/* Tuning switches of the process default context (per context: snrse_ctx_set_option; A/B experiments;
+ * the Python host also reads SNRSE_OPTS="name=value,..." at load):
  * "conv_variant" 0 auto, 1 register-staged v1, 2 LDS-DMA v2, 5 halo GEMM v5 (the default halo kernel);
  * "splitk" 0 disables the split-K small-image GEMMs, "splitk_target" workgroups a split launch aims for;
  * "epi_nt" 0 / 1 / 2 (auto above "epi_nt_mb" = 256 MB of output) non-temporal halo-GEMM output stores;
@@ -143,7 +159,7 @@ int snrse_temb_dense(const float* temb, const float* W, const float* bias, float
  * pyr [B*H*W][4] and out's GroupNorm statistics [B][SLOTS][128][2] (zeroed here unless option
  * stats_zeroed).  wgt: bf16 [128][64], k = (ky * 3 + kx) * 4 + channel, k >= 36 zero.
  * Requires W % 64 == 0 and (H * W / 64) % 16 == 0 (else SNRSE_EINVAL: use snrse_input_pack). */
-int snrse_input_conv(const void* x, const void* y, int B, int H, int W, const void* wgt, const float* bias,
+int snrse_input_conv(snrse_ctx* ctx, const void* x, const void* y, int B, int H, int W, const void* wgt, const float* bias,
                      void* out, float* pyr, double* stats, hipStream_t stream);
 
 /* Network input (ncsnpp.py:253-254, 282-285): complex x, y [B,F,T] -> im2col [B,F,T,64]

@@ -1,7 +1,12 @@
-// C-ABI housekeeping entries of libsnrse_hip.so (see include/snrse.h).
+// C-ABI housekeeping entries of libsnrse_hip.so (see include/snrse.h): version / error text / device
+// name, and the caller-owned launch contexts (snrse_ctx, common.h) with their switches.
 #include <hip/hip_runtime.h>
 
-extern "C" int snrse_abi_version(void) { return 1; }
+#include <new>
+
+#include "common.h"
+
+extern "C" int snrse_abi_version(void) { return 2; }
 
 extern "C" const char* snrse_error_string(int code) { return hipGetErrorString((hipError_t)code); }
 
@@ -19,6 +24,90 @@ extern "C" int snrse_device_name(char* buf, int len) {
   return 0;
 }
 
-// Library-wide switch behind the "stats_zeroed" option (declared in common.h, set through
-// snrse_set_option in conv.hip): statistics buffers arrive already zeroed.
-__attribute__((visibility("hidden"))) int g_snrse_stats_zeroed = 0;
+namespace {
+// The process default context: what a NULL context means, and what snrse_set_option /
+// snrse_set_workspace edit (single-stream callers; not reentrant).
+snrse_ctx g_default_ctx;
+
+bool name_is(const char* a, const char* b) {
+  int i = 0;
+  while (a[i] && a[i] == b[i]) ++i;
+  return a[i] == 0 && b[i] == 0;
+}
+
+// switch name -> field (nullptr: unknown)
+int* option_field(snrse_ctx& c, const char* name) {
+  if (name_is(name, "conv_variant")) return &c.conv_variant;
+  if (name_is(name, "splitk")) return &c.splitk;
+  if (name_is(name, "splitk_target")) return &c.splitk_target;
+  if (name_is(name, "epi_nt")) return &c.epi_nt;
+  if (name_is(name, "epi_nt_mb")) return &c.epi_nt_mb;
+  if (name_is(name, "h5_specialise")) return &c.h5_specialise;
+  if (name_is(name, "stats_zeroed")) return &c.stats_zeroed;
+  if (name_is(name, "resample_variant")) return &c.resample_variant;
+  if (name_is(name, "resample_nt")) return &c.resample_nt;
+  if (name_is(name, "resample_down_rows")) return &c.resample_down_rows;
+  return nullptr;
+}
+
+int set_option(snrse_ctx& c, const char* name, int value) {
+  if (!name) return SNRSE_EINVAL;
+  int* f = option_field(c, name);
+  if (!f) return SNRSE_EINVAL;
+  if (name_is(name, "splitk_target") || name_is(name, "epi_nt_mb")) value = value > 0 ? value : 256;
+  if (name_is(name, "stats_zeroed")) value = value ? 1 : 0;
+  *f = value;
+  return 0;
+}
+
+int get_option(const snrse_ctx& c, const char* name, int* value) {
+  if (!name || !value) return SNRSE_EINVAL;
+  if (const int* f = option_field(const_cast<snrse_ctx&>(c), name)) { *value = *f; return 0; }
+  if (name_is(name, "halo_kernel")) { *value = 5; return 0; }  // the halo generation variant 0 takes
+  if (name_is(name, "last_kernel")) { *value = c.last_kernel; return 0; }
+  if (name_is(name, "last_ksplit")) { *value = c.last_ksplit; return 0; }
+  if (name_is(name, "last_epi_nt")) { *value = c.last_epi_nt; return 0; }
+  if (name_is(name, "last_chunks")) { *value = c.last_chunks; return 0; }
+  return SNRSE_EINVAL;
+}
+
+int set_workspace(snrse_ctx& c, void* ptr, size_t bytes) {
+  if (!ptr && bytes) return SNRSE_EINVAL;
+  c.ws = (float*)ptr;
+  c.ws_bytes = ptr ? bytes : 0;
+  return 0;
+}
+}  // namespace
+
+__attribute__((visibility("hidden"))) snrse_ctx* snrse_ctx_resolve(snrse_ctx* c) { return c ? c : &g_default_ctx; }
+
+// A new context starts with the process default context's switches (so SNRSE_OPTS / snrse_set_option
+// settings made before carry over), no workspace and cleared read-backs.
+extern "C" snrse_ctx* snrse_ctx_create(void) {
+  snrse_ctx* c = new (std::nothrow) snrse_ctx(g_default_ctx);
+  if (!c) return nullptr;
+  c->ws = nullptr;
+  c->ws_bytes = 0;
+  c->last_kernel = 0;
+  c->last_ksplit = 1;
+  c->last_epi_nt = 0;
+  c->last_chunks = 1;
+  return c;
+}
+
+extern "C" void snrse_ctx_destroy(snrse_ctx* ctx) { delete ctx; }
+
+extern "C" int snrse_ctx_set_workspace(snrse_ctx* ctx, void* ptr, size_t bytes) {
+  return set_workspace(*snrse_ctx_resolve(ctx), ptr, bytes);
+}
+extern "C" int snrse_ctx_set_option(snrse_ctx* ctx, const char* name, int value) {
+  return set_option(*snrse_ctx_resolve(ctx), name, value);
+}
+extern "C" int snrse_ctx_get_option(const snrse_ctx* ctx, const char* name, int* value) {
+  return get_option(*snrse_ctx_resolve(const_cast<snrse_ctx*>(ctx)), name, value);
+}
+
+// Process-default forms (a NULL context): kept for single-stream callers and SNRSE_OPTS.
+extern "C" int snrse_set_workspace(void* ptr, size_t bytes) { return set_workspace(g_default_ctx, ptr, bytes); }
+extern "C" int snrse_set_option(const char* name, int value) { return set_option(g_default_ctx, name, value); }
+extern "C" int snrse_get_option(const char* name, int* value) { return get_option(g_default_ctx, name, value); }

@@ -72,9 +72,32 @@ enum { SNRSE_F32 = 0, SNRSE_BF16 = 1, SNRSE_F16 = 2, SNRSE_F64 = 3 };  // F16 / 
 // their atomics over the slots (a few hundred workgroups per image would otherwise queue on
 // the same 2*C addresses), consumers sum the slots.
 #define SNRSE_STAT_SLOTS 16
-// Option "stats_zeroed" (snrse_set_option): when 1 the caller hands over statistics buffers it
-// has already zeroed (one fill of a per-evaluation arena instead of a memset per producer).
-extern __attribute__((visibility("hidden"))) int g_snrse_stats_zeroed;
+
+// Caller-owned launch context (include/snrse.h `snrse_ctx`): the tuning switches, the split-K
+// workspace and the read-backs of the latest launch.  Host memory only.  The entries that take one
+// read and write nothing else, so calls with distinct contexts are independent (one context per
+// concurrently issuing host thread / stream); a NULL context means the process default one, which
+// snrse_set_option / snrse_set_workspace edit (abi.cpp).
+struct snrse_ctx {
+  // switches (names as in snrse_set_option)
+  int conv_variant = 0;        // 0 auto, 1 register-staged v1, 2 LDS-DMA v2, 5 halo v5
+  int splitk = 1;              // 0: no K splitting of the small-image GEMMs
+  int splitk_target = 256;     // workgroups a split-K launch aims for (C2 sweep: 256 best)
+  int epi_nt = 2;              // halo-GEMM non-temporal output stores: 0 off, 1 on, 2 above epi_nt_mb
+  int epi_nt_mb = 256;         // MB of output above which epi_nt = 2 streams (the Infinity Cache size)
+  int h5_specialise = 1;       // compile-time epilogue flags for the common bf16 configurations
+  int stats_zeroed = 0;        // statistics buffers arrive zeroed (the caller clears one arena)
+  int resample_variant = 0;    // 0 row-strip, 1 LDS-tiled gn_resample
+  int resample_nt = 0;         // non-temporal stores in gn_resample
+  int resample_down_rows = 2;  // output rows per down-sampling row strip (1, 2, 4)
+  // split-K workspace: [splits][M][Cout] f32 partial sums (NULL: no splitting)
+  float* ws = nullptr;
+  size_t ws_bytes = 0;
+  // read-backs of the latest launch through this context
+  int last_kernel = 0, last_ksplit = 1, last_epi_nt = 0, last_chunks = 1;
+};
+// `c`, or the process default context when c == NULL
+snrse_ctx* snrse_ctx_resolve(snrse_ctx* c);
 SNRSE_DEV size_t stat_idx(int b, int slot, int c, int C) {
   return (((size_t)b * SNRSE_STAT_SLOTS + slot) * C + c) * 2;
 }

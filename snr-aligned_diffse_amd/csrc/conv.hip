@@ -1083,41 +1083,31 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 #endif
 }
 
-int g_epi_nt_mb = 256;                // option "epi_nt_mb": output size (MB) above which epi_nt = 2 streams
-int g_epi_nt = 2;                     // option "epi_nt": non-temporal epilogue stores of the v5 halo GEMM:
-                                      // 0 off, 1 on, 2 when the output exceeds the 256 MB Infinity
-                                      // Cache (+1 % on the full-resolution convs)
-int g_last_epi_nt = 0;                // option read-back "last_epi_nt": store flavour of the latest v5 launch
-int g_last_chunks = 1;                // option read-back "last_chunks": launches of the latest snrse_conv2d
-int g_h5_specialise = 1;              // option "h5_specialise": compile-time epilogue flags for the common
-                                      // bf16 configurations (0: the run-time flags everywhere)
-
 template <typename TO, int GNM, int EF>
 int launch_halo5_ef(ConvParams p, int grid, size_t lds, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    SNRSE_RET(hipFuncSetAttribute((const void*)conv_halo5_kernel<TO, GNM, EF>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_halo5_kernel<TO, GNM, EF>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  SNRSE_RET(attr);  // (thread-safe one-time set: a function-local static)
   hipLaunchKernelGGL((conv_halo5_kernel<TO, GNM, EF>), dim3(grid), dim3(256), lds, s, p);
   return (int)hipGetLastError();
 }
 
 template <typename TO, int GNM>
-int launch_halo5_gn(ConvParams p, hipStream_t s) {
+int launch_halo5_gn(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   // halo + weight ring + (stamps build: 4 x 32 stamps) + the next chunk's GroupNorm affine (2 x 32 f32)
   constexpr size_t lds = 396 * 64 + 2 * 3 * 128 * 64 + 1024 + 256;
   p.ntn = p.Cout / 128;
-  p.epi_nt = g_epi_nt == 2 ? ((long long)p.M * p.out_ld * (long long)sizeof(TO) > ((long long)g_epi_nt_mb << 20))
-                           : g_epi_nt;
-  g_last_epi_nt = p.epi_nt;
+  // non-temporal output stores when the output exceeds the 256 MB Infinity Cache (+1 % on the
+  // full-resolution convs)
+  p.epi_nt = cx.epi_nt == 2 ? ((long long)p.M * p.out_ld * (long long)sizeof(TO) > ((long long)cx.epi_nt_mb << 20))
+                            : cx.epi_nt;
+  cx.last_epi_nt = p.epi_nt;
   const int tiles = p.B * (p.H / 4) * (p.W / 64) * p.ntn;
   const int grid = tiles;
   // the bf16 ResBlock configurations of the NCSN++ path get a branch-free epilogue (bias always on):
   // Conv_0 (+temb), Conv_1 (+residual | +1x1 shortcut as extra K | +Combine), each +-stats, +-NT
   if constexpr (sizeof(TO) == 2 && GNM != 1) {
-    if (g_h5_specialise && p.bias) {
+    if (cx.h5_specialise && p.bias) {
       switch (epi_flags(p)) {
 #define SNRSE_H5_EF(F) \
   case (F): return launch_halo5_ef<TO, GNM, (F)>(p, grid, lds, s);
@@ -1139,28 +1129,22 @@ int launch_halo5_gn(ConvParams p, hipStream_t s) {
 
 // GroupNorm prologue mode as a template argument: the halo transform is straight-line code
 template <typename TO>
-int launch_halo5(ConvParams p, hipStream_t s) {
-  if (!p.gn_scale) return launch_halo5_gn<TO, 0>(p, s);
-  if (!p.gn_act) return launch_halo5_gn<TO, 1>(p, s);
-  return launch_halo5_gn<TO, 2>(p, s);
+int launch_halo5(ConvParams p, hipStream_t s, snrse_ctx& cx) {
+  if (!p.gn_scale) return launch_halo5_gn<TO, 0>(p, s, cx);
+  if (!p.gn_act) return launch_halo5_gn<TO, 1>(p, s, cx);
+  return launch_halo5_gn<TO, 2>(p, s, cx);
 }
-
-float* g_ws = nullptr;   // split-K workspace (snrse_set_workspace)
-size_t g_ws_bytes = 0;
-int g_splitk = 1;        // option "splitk": 0 disables K splitting
-int g_splitk_target = 256;  // option "splitk_target": workgroups a split-K launch aims for (swept
-                            // 128/192/256/512/1024 on C2: 256 best, split-K off is 9 % slower)
-int g_last_ksplit = 1;   // option read-back "last_ksplit": splits of the latest v2 launch
 
 // K splits for a v2 launch of `tiles` output tiles over nk K-tiles: about one workgroup per CU when
 // the tile grid alone underfills the chip (the small NCSN++ levels), >= 4 K-tiles per split, and
 // the partial sums within the registered workspace
-int choose_ksplit(const ConvParams& p, int tiles, int nk, int min_kt = 4) {
-  if (!g_splitk || !g_ws || tiles >= g_splitk_target * 3 / 4) return 1;
-  int s = (g_splitk_target + tiles - 1) / tiles;
+// (splitk_target 128/192/256/512/1024 swept on C2: 256 best, split-K off is 9 % slower)
+int choose_ksplit(const ConvParams& p, int tiles, int nk, const snrse_ctx& cx, int min_kt = 4) {
+  if (!cx.splitk || !cx.ws || tiles >= cx.splitk_target * 3 / 4) return 1;
+  int s = (cx.splitk_target + tiles - 1) / tiles;
   if (s > nk / min_kt) s = nk / min_kt;
   const size_t plane = (size_t)p.M * p.Cout * sizeof(float);
-  if ((size_t)s * plane > g_ws_bytes) s = (int)(g_ws_bytes / plane);
+  if ((size_t)s * plane > cx.ws_bytes) s = (int)(cx.ws_bytes / plane);
   return s >= 2 ? s : 1;
 }
 
@@ -1168,14 +1152,14 @@ int choose_ksplit(const ConvParams& p, int tiles, int nk, int min_kt = 4) {
 // grid underfills the chip (the low-resolution NCSN++ levels: 4-60 workgroups at 30 s, C5) split K
 // across workgroups (>= 2 K-tiles each) and finish in conv_splitk_finalize.
 template <typename T, typename TO, int BM, int BN, int WM, int WN>
-int launch_conv(ConvParams p, int npad, hipStream_t s) {
+int launch_conv(ConvParams p, int npad, hipStream_t s, snrse_ctx& cx) {
   using Tr = ConvTraits<T>;
   p.ntn = npad / BN;
   const int tiles = ((p.M + BM - 1) / BM) * p.ntn;
   const int nk = p.ksize * p.ksize * ((p.C0 + p.C1) / Tr::KT) + (p.sc_src ? (p.Csc + p.Csc1) / Tr::KT : 0);
-  p.ksplit = (sizeof(T) == 4 && BN == 128 && p.Cout % 128 == 0) ? choose_ksplit(p, tiles, nk, 2) : 1;
-  p.ws = g_ws;
-  g_last_ksplit = p.ksplit;
+  p.ksplit = (sizeof(T) == 4 && BN == 128 && p.Cout % 128 == 0) ? choose_ksplit(p, tiles, nk, cx, 2) : 1;
+  p.ws = cx.ws;
+  cx.last_ksplit = p.ksplit;
   const size_t lds = (size_t)2 * (BM + BN) * 128;
   hipLaunchKernelGGL((conv_mfma_kernel<T, TO, BM, BN, WM, WN>), dim3(tiles * p.ksplit), dim3(64 * WM * WN), lds, s, p);
   if (p.ksplit > 1) {
@@ -1188,20 +1172,17 @@ int launch_conv(ConvParams p, int npad, hipStream_t s) {
 }
 
 template <int BM, int BN, typename TO>
-int launch_glds(ConvParams p, hipStream_t s) {
+int launch_glds(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   constexpr size_t lds = (size_t)3 * (BM + BN) * 128;
-  static bool attr = false;
-  if (!attr) {
-    SNRSE_RET(hipFuncSetAttribute((const void*)conv_glds_kernel<BM, BN, TO>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_glds_kernel<BM, BN, TO>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  SNRSE_RET(attr);
   p.ntn = p.Cout / BN;
   const int ntm = (p.M + BM - 1) / BM;
   const int nk = p.ksize * p.ksize * ((p.C0 + p.C1) / 64) + (p.sc_src ? (p.Csc + p.Csc1) / 64 : 0);
-  p.ksplit = choose_ksplit(p, ntm * p.ntn, nk);
-  p.ws = g_ws;
-  g_last_ksplit = p.ksplit;
+  p.ksplit = choose_ksplit(p, ntm * p.ntn, nk, cx);
+  p.ws = cx.ws;
+  cx.last_ksplit = p.ksplit;
   hipLaunchKernelGGL((conv_glds_kernel<BM, BN, TO>), dim3(ntm * p.ntn * p.ksplit), dim3(512), lds, s, p);
   if (p.ksplit > 1) {
     SNRSE_LAUNCH_CHECK();
@@ -1215,47 +1196,45 @@ int launch_glds(ConvParams p, hipStream_t s) {
 // 0 auto, 1 force v1 (register-staged), 2 force v2 (no halo), 5 halo v5; the experimental
 // v3/v4/v6/v7/v8/v9 generations (none faster than v5 on the NCSN++ shapes: profiles/r02d_h7_ablations.json,
 // profiles/r02g_conv_bench_v5_v7_v9.jsonl) live in git history and tools/experimental/, outside the product library
-int g_conv_variant = 0;
 constexpr int kHaloAuto = 5;  // halo kernel generation taken by variant 0 (fastest measured: profiles/)
-int g_last_kernel = 0;        // option read-back "last_kernel": generation of the latest launch (10 = head)
 
 template <typename T, typename TO>
-int dispatch_conv(const ConvParams& p, hipStream_t s) {
+int dispatch_conv(const ConvParams& p, hipStream_t s, snrse_ctx& cx) {
   if (p.Cout >= 64) {
     if (p.Cout % 128 != 0) return SNRSE_EINVAL;
     if constexpr (sizeof(T) == 2) {
       const bool fits = p.bytes0 < 0x7ff00000ll && p.bytes1 < 0x7ff00000ll && p.sc_bytes0 < 0x7ff00000ll &&
                         p.sc_bytes1 < 0x7ff00000ll;
-      if (g_conv_variant != 1 && fits) {
-        if (g_conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0) {
-          g_last_kernel = kHaloAuto;
-          return launch_halo5<TO>(p, s);
+      if (cx.conv_variant != 1 && fits) {
+        if (cx.conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0) {
+          cx.last_kernel = kHaloAuto;
+          return launch_halo5<TO>(p, s, cx);
         }
         if (p.gn_scale) return SNRSE_EINVAL;  // fused GroupNorm exists only on the halo paths
-        g_last_kernel = 2;
-        if (p.Cout % 256 == 0) return launch_glds<128, 256, TO>(p, s);
-        return launch_glds<256, 128, TO>(p, s);
+        cx.last_kernel = 2;
+        if (p.Cout % 256 == 0) return launch_glds<128, 256, TO>(p, s, cx);
+        return launch_glds<256, 128, TO>(p, s, cx);
       }
     }
     if (p.gn_scale) return SNRSE_EINVAL;
-    g_last_kernel = 1;
-    return launch_conv<T, TO, 128, 128, 2, 2>(p, p.Cout, s);
+    cx.last_kernel = 1;
+    return launch_conv<T, TO, 128, 128, 2, 2>(p, p.Cout, s, cx);
   }
   if constexpr (sizeof(T) == 2 && sizeof(TO) == 4) {
-    if (g_conv_variant != 1 && head_ok(p)) {
-      g_last_kernel = 10;
+    if (cx.conv_variant != 1 && head_ok(p)) {
+      cx.last_kernel = 10;
       return launch_head(p, s);
     }
   }
   if (p.gn_scale) return SNRSE_EINVAL;
   if (p.Cout > 16) return SNRSE_EINVAL;
-  g_last_kernel = 1;
-  return launch_conv<T, TO, 128, 16, 4, 1>(p, 16, s);
+  cx.last_kernel = 1;
+  return launch_conv<T, TO, 128, 16, 4, 1>(p, 16, s, cx);
 }
 
 }  // namespace
 
-extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, int B, int H, int W,
+extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void* src1, int C1, int B, int H, int W,
                             int ksize, const void* wgt, const void* sc_src, int Csc, const void* sc_src1,
                             int Csc1, const void* sc_wgt,
                             const float* bias, const float* temb, int temb_stride, const void* res,
@@ -1265,6 +1244,7 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
                             int out_f32, hipStream_t stream) {
   using TrB = ConvTraits<bf16_t>;
   using TrF = ConvTraits<float>;
+  snrse_ctx& cx = *snrse_ctx_resolve(ctx);
   const int KT = dtype == SNRSE_BF16 ? TrB::KT : TrF::KT;
   if (!src0 || !wgt || !out || (ksize != 1 && ksize != 3)) return SNRSE_EINVAL;
   if (C0 % KT || C1 % KT || (sc_src && (Csc % KT || Csc1 % KT))) return SNRSE_EINVAL;
@@ -1298,12 +1278,12 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
   p.wbytes = (long long)npad * ksize * ksize * (C0 + C1) * esz;
   p.sc_wbytes = (long long)npad * (p.Csc + p.Csc1) * esz;
   p.ntn = 1;
-  if (stats && !g_snrse_stats_zeroed) SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * Cout, stream));
+  if (stats && !cx.stats_zeroed) SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * Cout, stream));
   if (dtype != SNRSE_BF16 && dtype != SNRSE_F32) return SNRSE_EINVAL;
   auto run = [&](const ConvParams& q) {
     if (dtype == SNRSE_BF16)
-      return out_f32 ? dispatch_conv<bf16_t, float>(q, stream) : dispatch_conv<bf16_t, bf16_t>(q, stream);
-    return dispatch_conv<float, float>(q, stream);
+      return out_f32 ? dispatch_conv<bf16_t, float>(q, stream, cx) : dispatch_conv<bf16_t, bf16_t>(q, stream, cx);
+    return dispatch_conv<float, float>(q, stream, cx);
   };
   // The buffer-resource kernels address each source with a 32-bit byte extent and offset.  Images are
   // independent (NHWC, batch outermost), so a batch whose sources exceed 2 GiB (e.g. B >= 64 at the
@@ -1311,10 +1291,10 @@ extern "C" int snrse_conv2d(const void* src0, int C0, const void* src1, int C1, 
   // never a silent fallback to the register-staged GEMM.
   const long long per_img = (long long)H * W * std::max(std::max(C0, C1), std::max(p.Csc, p.Csc1)) * esz;
   constexpr long long kLim = 0x7ff00000ll;
-  g_last_chunks = 1;
+  cx.last_chunks = 1;
   if (per_img * B < kLim || per_img >= kLim) return run(p);
   const int chunk = (int)((kLim - 1) / per_img);
-  g_last_chunks = (B + chunk - 1) / chunk;
+  cx.last_chunks = (B + chunk - 1) / chunk;
   const long long HWl = (long long)H * W;
   for (int b0 = 0; b0 < B; b0 += chunk) {
     const int nb = std::min(chunk, B - b0);
@@ -1352,56 +1332,3 @@ extern "C" int snrse_debug_set_stamps(void* buf) {
   return 0;
 }
 #endif
-
-extern __attribute__((visibility("hidden"))) int g_resample_variant, g_resample_nt, g_resample_down_rows;  // resample.hip
-
-static bool name_is(const char* a, const char* b) {
-  int i = 0;
-  while (a[i] && a[i] == b[i]) ++i;
-  return a[i] == 0 && b[i] == 0;
-}
-
-extern "C" int snrse_get_option(const char* name, int* value) {
-  if (!name || !value) return SNRSE_EINVAL;
-  if (name_is(name, "conv_variant")) { *value = g_conv_variant; return 0; }
-  if (name_is(name, "halo_kernel")) {  // generation taken by a halo-eligible bf16 conv
-    *value = g_conv_variant == 0 ? kHaloAuto : 5;
-    return 0;
-  }
-  if (name_is(name, "last_kernel")) { *value = g_last_kernel; return 0; }
-  if (name_is(name, "splitk")) { *value = g_splitk; return 0; }
-  if (name_is(name, "splitk_target")) { *value = g_splitk_target; return 0; }
-  if (name_is(name, "epi_nt")) { *value = g_epi_nt; return 0; }
-  if (name_is(name, "epi_nt_mb")) { *value = g_epi_nt_mb; return 0; }
-  if (name_is(name, "h5_specialise")) { *value = g_h5_specialise; return 0; }
-  if (name_is(name, "stats_zeroed")) { *value = g_snrse_stats_zeroed; return 0; }
-  if (name_is(name, "last_ksplit")) { *value = g_last_ksplit; return 0; }
-  if (name_is(name, "last_epi_nt")) { *value = g_last_epi_nt; return 0; }
-  if (name_is(name, "last_chunks")) { *value = g_last_chunks; return 0; }
-  if (name_is(name, "resample_variant")) { *value = g_resample_variant; return 0; }
-  if (name_is(name, "resample_nt")) { *value = g_resample_nt; return 0; }
-  if (name_is(name, "resample_down_rows")) { *value = g_resample_down_rows; return 0; }
-  return SNRSE_EINVAL;
-}
-
-extern "C" int snrse_set_option(const char* name, int value) {
-  if (!name) return SNRSE_EINVAL;
-  if (name_is(name, "conv_variant")) { g_conv_variant = value; return 0; }
-  if (name_is(name, "splitk")) { g_splitk = value; return 0; }
-  if (name_is(name, "splitk_target")) { g_splitk_target = value > 0 ? value : 256; return 0; }
-  if (name_is(name, "epi_nt")) { g_epi_nt = value; return 0; }
-  if (name_is(name, "epi_nt_mb")) { g_epi_nt_mb = value > 0 ? value : 256; return 0; }
-  if (name_is(name, "h5_specialise")) { g_h5_specialise = value; return 0; }
-  if (name_is(name, "stats_zeroed")) { g_snrse_stats_zeroed = value ? 1 : 0; return 0; }
-  if (name_is(name, "resample_variant")) { g_resample_variant = value; return 0; }
-  if (name_is(name, "resample_nt")) { g_resample_nt = value; return 0; }
-  if (name_is(name, "resample_down_rows")) { g_resample_down_rows = value; return 0; }
-  return SNRSE_EINVAL;
-}
-
-extern "C" int snrse_set_workspace(void* ptr, size_t bytes) {
-  if (!ptr && bytes) return SNRSE_EINVAL;
-  g_ws = (float*)ptr;
-  g_ws_bytes = ptr ? bytes : 0;
-  return 0;
-}

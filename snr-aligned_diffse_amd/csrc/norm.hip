@@ -276,13 +276,14 @@ extern "C" int snrse_gn_scale_shift(const double* sums0, int C0, const double* s
   return (int)hipGetLastError();
 }
 
-extern "C" int snrse_gn_stats(const void* src0, int C0, const void* src1, int C1, int B, int HW,
+extern "C" int snrse_gn_stats(snrse_ctx* ctx, const void* src0, int C0, const void* src1, int C1, int B, int HW,
                               double* sums, double* sums1, int dtype, hipStream_t stream) {
   const int V = dtype == SNRSE_BF16 ? 8 : 4;
   const int C = C0 + C1;
   if (C % V || C0 % V || C / V > 256 || !sums || (C1 > 0 && !sums1)) return SNRSE_EINVAL;
-  if (!g_snrse_stats_zeroed) SNRSE_RET(hipMemsetAsync(sums, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * C0 * B, stream));
-  if (C1 > 0 && !g_snrse_stats_zeroed) SNRSE_RET(hipMemsetAsync(sums1, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * C1 * B, stream));
+  const bool zeroed = snrse_ctx_resolve(ctx)->stats_zeroed != 0;
+  if (!zeroed) SNRSE_RET(hipMemsetAsync(sums, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * C0 * B, stream));
+  if (C1 > 0 && !zeroed) SNRSE_RET(hipMemsetAsync(sums1, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * C1 * B, stream));
   int nblk = (HW + 1023) / 1024;
   if (nblk > 256) nblk = 256;
   const int ppb = (HW + nblk - 1) / nblk;

@@ -15,11 +15,9 @@
 
 #include <type_traits>
 
-// option "resample_variant" (snrse_set_option): 0 auto (row strips where C / 8 divides 64), 1 tiled
-__attribute__((visibility("hidden"))) int g_resample_variant = 0;
-__attribute__((visibility("hidden"))) int g_resample_down_rows = 2;  // option "resample_down_rows": output rows per down strip (1, 2, 4)
-// option "resample_nt": 1 = non-temporal stores in the row-strip kernel
-__attribute__((visibility("hidden"))) int g_resample_nt = 0;
+// switches (snrse_ctx, common.h): "resample_variant" 0 auto (row strips where C / 8 divides 64), 1 tiled;
+// "resample_down_rows" output rows per down strip (1, 2, 4); "resample_nt" 1 = non-temporal stores in the
+// row-strip kernel
 
 namespace {
 
@@ -474,7 +472,7 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
 
 template <int MODE, int NV, int CPT, int RD = 1>
 int launch_rows(const void* src, int B, int H, int W, const float* scale, const float* shift, int act, void* out_act,
-                void* out_raw, hipStream_t stream) {
+                void* out_raw, hipStream_t stream, int nt) {
   const int nrows = MODE == MODE_DOWN ? H / 2 / RD : 2 * H;  // strips per column segment
   const int span = MODE == MODE_DOWN ? W / 2 : W;  // positions a strip walks (output cols / input cols)
   // strip length: 16 positions, shortened on small images until the grid has >= 2^17 threads (8 waves
@@ -489,7 +487,7 @@ int launch_rows(const void* src, int B, int H, int W, const float* scale, const 
     return SNRSE_EINVAL;
   hipLaunchKernelGGL((gn_resample_rows_kernel<MODE, NV, CPT, RD>), dim3((unsigned)nblk), dim3(256), 0, stream,
                      (const bf16_t*)src, H, W, L, nseg, nrows, scale, shift, act, (bf16_t*)out_act, (bf16_t*)out_raw,
-                     (int)nblk, B, (int)sp_img, g_resample_nt);
+                     (int)nblk, B, (int)sp_img, nt);
   return (int)hipGetLastError();
 }
 
@@ -497,38 +495,38 @@ int launch_rows(const void* src, int B, int H, int W, const float* scale, const 
 // up: 8 channels per lane (16-B stores)
 template <int MODE, int RD>
 int dispatch_rows_rd(const void* src, int C, int B, int H, int W, const float* scale, const float* shift, int act,
-                     void* out_act, void* out_raw, hipStream_t stream) {
+                     void* out_act, void* out_raw, hipStream_t stream, int nt) {
   constexpr int CPT = MODE == MODE_DOWN ? 4 : 8;
   if (C % CPT) return -1;
   switch (C / CPT) {
-    case 1: return launch_rows<MODE, 1, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
-    case 2: return launch_rows<MODE, 2, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
-    case 4: return launch_rows<MODE, 4, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
-    case 8: return launch_rows<MODE, 8, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
-    case 16: return launch_rows<MODE, 16, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
-    case 32: return launch_rows<MODE, 32, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
-    case 64: return launch_rows<MODE, 64, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    case 1: return launch_rows<MODE, 1, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
+    case 2: return launch_rows<MODE, 2, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
+    case 4: return launch_rows<MODE, 4, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
+    case 8: return launch_rows<MODE, 8, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
+    case 16: return launch_rows<MODE, 16, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
+    case 32: return launch_rows<MODE, 32, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
+    case 64: return launch_rows<MODE, 64, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
     default: return -1;  // not handled here
   }
 }
 template <int MODE>
 int dispatch_rows(const void* src, int C, int B, int H, int W, const float* scale, const float* shift, int act,
-                  void* out_act, void* out_raw, hipStream_t stream) {
+                  void* out_act, void* out_raw, hipStream_t stream, const snrse_ctx& cx) {
   if constexpr (MODE == MODE_DOWN) {
     const int Ho = H / 2;
-    if (g_resample_down_rows >= 4 && Ho % 4 == 0)
-      return dispatch_rows_rd<MODE, 4>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream);
-    if (g_resample_down_rows >= 2 && Ho % 2 == 0)
-      return dispatch_rows_rd<MODE, 2>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    if (cx.resample_down_rows >= 4 && Ho % 4 == 0)
+      return dispatch_rows_rd<MODE, 4>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx.resample_nt);
+    if (cx.resample_down_rows >= 2 && Ho % 2 == 0)
+      return dispatch_rows_rd<MODE, 2>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx.resample_nt);
   }
-  return dispatch_rows_rd<MODE, 1>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream);
+  return dispatch_rows_rd<MODE, 1>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx.resample_nt);
 }
 
 template <int MODE>
 int launch_resample(const void* src, int C, int B, int H, int W, const float* scale, const float* shift, int act,
-                    void* out_act, void* out_raw, hipStream_t stream) {
-  if (g_resample_variant == 0) {
-    const int r = dispatch_rows<MODE>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream);
+                    void* out_act, void* out_raw, hipStream_t stream, const snrse_ctx& cx) {
+  if (cx.resample_variant == 0) {
+    const int r = dispatch_rows<MODE>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx);
     if (r >= 0) return r;
   }
   if (C % kCB) return SNRSE_EINVAL;
@@ -544,16 +542,17 @@ int launch_resample(const void* src, int C, int B, int H, int W, const float* sc
 
 }  // namespace
 
-extern "C" int snrse_gn_resample(const void* src, int C, int B, int H, int W, const float* scale,
+extern "C" int snrse_gn_resample(snrse_ctx* ctx, const void* src, int C, int B, int H, int W, const float* scale,
                                  const float* shift, int act, int mode, void* out_act, void* out_raw,
                                  hipStream_t stream) {
   if (!src || !out_act || C <= 0 || C % 8 || B <= 0 || H <= 0 || W <= 0 || (!scale) != (!shift))
     return SNRSE_EINVAL;
   if (mode == MODE_DOWN) {
     if ((H & 1) || (W & 1)) return SNRSE_EINVAL;
-    return launch_resample<MODE_DOWN>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream);
+    return launch_resample<MODE_DOWN>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, *snrse_ctx_resolve(ctx));
   }
-  if (mode == MODE_UP) return launch_resample<MODE_UP>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream);
+  if (mode == MODE_UP)
+    return launch_resample<MODE_UP>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, *snrse_ctx_resolve(ctx));
   return SNRSE_EINVAL;
 }
 

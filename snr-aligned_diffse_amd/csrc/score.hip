@@ -442,12 +442,12 @@ extern "C" int snrse_temb_dense(const float* temb, const float* W, const float* 
   return 0;
 }
 
-extern "C" int snrse_input_conv(const void* x, const void* y, int B, int H, int W, const void* wgt, const float* bias,
+extern "C" int snrse_input_conv(snrse_ctx* ctx, const void* x, const void* y, int B, int H, int W, const void* wgt, const float* bias,
                                 void* out, float* pyr, double* stats, hipStream_t s) {
   if (B <= 0 || H <= 0 || W <= 0 || W % 64 || ((long long)H * W / 64) % 16 || !x || !y || !wgt || !bias || !out ||
       !pyr || !stats)
     return SNRSE_EINVAL;
-  if (!g_snrse_stats_zeroed)
+  if (!snrse_ctx_resolve(ctx)->stats_zeroed)
     SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * 128, s));
   const long long blocks = (long long)B * H * W / (64 * 16);
   hipLaunchKernelGGL(input_conv_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const float2*)x, (const float2*)y,

@@ -23,10 +23,10 @@ _vp, _i, _f, _u64, _ll = C.c_void_p, C.c_int, C.c_float, C.c_uint64, C.c_longlon
 # name -> argtypes (all return int status except the housekeeping ones)
 SIGNATURES = {
     "snrse_upfirdn2d": [_vp, _vp, _vp] + [_i] * 15 + [_vp],
-    "snrse_conv2d": [_vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _i, _vp, _i, _f,
+    "snrse_conv2d": [_vp, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp, _i, _vp, _i, _f,
                      _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _i, _i, _i, _vp],
     "snrse_gn_scale_shift": [_vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _f, _vp, _vp, _vp],
-    "snrse_gn_stats": [_vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _vp],
+    "snrse_gn_stats": [_vp, _vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _vp],
     "snrse_gn_apply": [_vp, _i, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _f, _i, _i, _vp, _i, _vp],
     "snrse_set_option": [C.c_char_p, _i],
     "snrse_get_option": [C.c_char_p, _vp],
@@ -40,13 +40,17 @@ SIGNATURES = {
     "snrse_stft": [_vp, _i, _i, _vp, _f, _i, _i, _vp, _vp],
     "snrse_absmax": [_vp, _i, _i, _vp, _vp],
     "snrse_energy_ratios": [_vp, _vp, _vp, _i, _i, _vp, _vp],
-    "snrse_input_conv": [_vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "snrse_input_conv": [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
     "snrse_spec_transform": [_vp, _vp, C.c_longlong, _i, _vp],
     "snrse_snrnet": [_vp, _i, _i] + [_vp] * 17 + [_vp, _vp, _vp],
     "snrse_istft": [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
-    "snrse_gn_resample": [_vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp],
+    "snrse_gn_resample": [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp],
     "snrse_gn_act": [_vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp],
     "snrse_set_workspace": [_vp, C.c_size_t],
+    # caller-owned launch contexts (snrse_ctx: switches, split-K workspace, read-backs)
+    "snrse_ctx_set_workspace": [_vp, _vp, C.c_size_t],
+    "snrse_ctx_set_option": [_vp, C.c_char_p, _i],
+    "snrse_ctx_get_option": [_vp, C.c_char_p, _vp],
     # consistency-training step (csrc/train.hip)
     "snrse_conv_wgrad": [_vp, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp],
     "snrse_chan_sum": [_vp, _i, _i, _i, _vp, _vp, _f, _vp],
@@ -65,7 +69,8 @@ SIGNATURES = {
     "snrse_adam_ema": [_vp, _vp, _vp, _i, _f, _f, _f, _f, _f, _f, _f, _vp],
 }
 HOUSEKEEPING = {"snrse_abi_version": ([], _i), "snrse_error_string": ([_i], C.c_char_p),
-                "snrse_device_name": ([C.c_char_p, _i], _i), "snrse_snrnet_workspace": ([_i, _i], C.c_size_t)}
+                "snrse_device_name": ([C.c_char_p, _i], _i), "snrse_snrnet_workspace": ([_i, _i], C.c_size_t),
+                "snrse_ctx_create": ([], _vp), "snrse_ctx_destroy": ([_vp], None)}
 
 _lib = None
 

@@ -2,17 +2,24 @@
 
 Every op requires HIP device tensors and raises otherwise — there is no CPU fallback.
 
-Concurrency contract: ONE stream per process runs network evaluations.  Two pieces of state are
-process-wide and ordered only by that stream: the split-K workspace (_WS / the library's g_ws) and
-each network's StatsArena (zeroed on the current stream when an evaluation starts).  Running two
-evaluations concurrently on different streams would race on both; the multi-GPU path uses one
-process per GPU, so it never does.
+Concurrency contract.  The library's stateful entries (snrse_conv2d, snrse_gn_stats, snrse_input_conv,
+snrse_gn_resample) take a caller-owned launch context (snrse_ctx: switches, split-K workspace, read-backs
+of the latest launch), so calls through distinct contexts are independent.  Here every host thread has
+its own context per device (LaunchContext, thread-local, with its own split-K workspace), the StatsArena
+stack is thread-local, and each network keeps one arena per launch stream.  So evaluations issued by
+different host threads on different streams run concurrently without sharing mutable state, and one
+thread interleaving several streams (snrse.sampler.pc_sample_lockstep) switches to a per-lane context
+with use_workspace_lane(lane) before issuing each lane's launches.  set_option() is process-wide policy:
+it edits the library's process default and every live context; get_option() reads the calling thread's
+current context (so "last_kernel" etc. describe that thread's latest launch).
 """
 from __future__ import annotations
 
 import ctypes as C
 import math
 import os
+import threading
+import weakref
 
 import torch
 
@@ -38,38 +45,83 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-_WS = {"dev": None, "buf": None, "lane": 0, "bufs": {}}
-
-
 def _ws_alloc(dev):
     mb = int(os.environ.get("SNRSE_WORKSPACE_MB", "128"))
     return (torch.empty(mb << 18, dtype=torch.float32, device=dev) if mb > 0 else None), mb
 
 
-def _workspace(dev):
-    """Register (once per device) the split-K workspace of the small-image GEMMs
-    (snrse_set_workspace); SNRSE_WORKSPACE_MB sizes it, 0 disables K splitting."""
-    if _WS["dev"] == dev:
-        return
-    buf, mb = _ws_alloc(dev)
-    _lib.call("snrse_set_workspace", None if buf is None else buf.data_ptr(), 0 if buf is None else mb << 20)
-    _WS.update(dev=dev, buf=buf, lane=0, bufs={0: buf})
+_CONTEXTS = weakref.WeakSet()  # every live LaunchContext (set_option reaches all of them)
+_TLS = threading.local()       # per thread: {device: {lane: LaunchContext}}, current lane per device, arenas
+
+
+class LaunchContext:
+    """A caller-owned snrse_ctx (include/snrse.h) on one device: the library's switches (copied from the
+    process default at creation), a split-K workspace of SNRSE_WORKSPACE_MB (default 128; 0 disables K
+    splitting) and the read-backs of the latest launch issued through it."""
+
+    def __init__(self, device):
+        lib = _lib.load()
+        self.device = torch.device(device)
+        self.ptr = lib.snrse_ctx_create()
+        if not self.ptr:
+            raise MemoryError("snrse_ctx_create failed")
+        self._lib = lib
+        self.ws, mb = _ws_alloc(self.device)
+        _lib.call("snrse_ctx_set_workspace", self.ptr, None if self.ws is None else self.ws.data_ptr(),
+                  0 if self.ws is None else mb << 20)
+        self.zeroed = 0  # mirror of the context's "stats_zeroed" switch
+        _CONTEXTS.add(self)
+
+    def set_option(self, name, value):
+        _lib.call("snrse_ctx_set_option", self.ptr, name.encode(), int(value))
+        if name == "stats_zeroed":
+            self.zeroed = int(bool(value))
+
+    def get_option(self, name):
+        v = C.c_int(0)
+        _lib.call("snrse_ctx_get_option", self.ptr, name.encode(), C.addressof(v))
+        return v.value
+
+    def __del__(self):
+        try:
+            self._lib.snrse_ctx_destroy(self.ptr)
+        except Exception:
+            pass
+
+
+def _tls_contexts(dev):
+    d = getattr(_TLS, "ctx", None)
+    if d is None:
+        d = _TLS.ctx = {}
+        _TLS.lane = {}
+    return d.setdefault(torch.device(dev), {})
+
+
+def context(dev=None, lane=None):
+    """The calling thread's current LaunchContext on `dev` (lane: that lane's context, created on first
+    use; default: the lane selected by use_workspace_lane, initially 0)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if dev is None else torch.device(dev)
+    ctxs = _tls_contexts(dev)
+    if lane is None:
+        lane = _TLS.lane.get(dev, 0)
+    c = ctxs.get(lane)
+    if c is None:
+        c = ctxs[lane] = LaunchContext(dev)
+    return c
+
+
+def _cx(dev):
+    return context(dev).ptr
 
 
 def use_workspace_lane(lane, dev):
-    """Point the library's split-K workspace at lane `lane`'s own buffer (allocated on first use).
-    The two-stream sampler (snrse.sampler.pc_sample_lockstep) issues each half-batch's launches
-    behind its lane's workspace, so concurrent split-K GEMMs on different streams never share one."""
-    _workspace(dev)
-    if _WS["lane"] == lane:
-        return
-    buf = _WS["bufs"].get(lane)
-    if buf is None and lane not in _WS["bufs"]:
-        buf, _ = _ws_alloc(dev)
-        _WS["bufs"][lane] = buf
-    mb = 0 if buf is None else buf.numel() * 4 >> 20
-    _lib.call("snrse_set_workspace", None if buf is None else buf.data_ptr(), mb << 20)
-    _WS.update(buf=buf, lane=lane)
+    """Make lane `lane`'s own context (and so its own split-K workspace and read-backs) the calling
+    thread's current one on `dev`.  The two-stream sampler (snrse.sampler.pc_sample_lockstep) issues each
+    half-batch's launches behind its lane's context, so concurrent split-K GEMMs never share a workspace."""
+    dev = torch.device(dev)
+    _tls_contexts(dev)
+    _TLS.lane[dev] = lane
+    context(dev, lane)
 
 
 def _dev(*ts):
@@ -88,7 +140,7 @@ def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_w
     stats: optional new_stats() buffer receiving the output's per-channel (sum, sumsq).
     gn: optional (scale, shift) [B, C0+C1] f32 — consume SiLU(GN(x)) (halo path only, see halo_ok)."""
     _dev(src0, src1, wgt, sc, sc1, sc_wgt, bias, res, comb, comb_w, comb_b, temb)
-    _workspace(src0.device)
+    cx = context(src0.device)
     B, H, W, C0 = src0.shape
     C1 = 0 if src1 is None else src1.shape[3]
     Csc = 0 if sc is None else sc.shape[3]
@@ -96,8 +148,8 @@ def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_w
     odt = torch.float32 if out_f32 else src0.dtype
     if out is None:
         out = torch.empty(B, H, W, cout, device=src0.device, dtype=odt)
-    _stats_zeroed(stats)
-    _lib.call("snrse_conv2d", _ptr(src0), C0, _ptr(src1), C1, B, H, W, ksize, _ptr(wgt), _ptr(sc), Csc,
+    _stats_zeroed(cx, stats)
+    _lib.call("snrse_conv2d", cx.ptr, _ptr(src0), C0, _ptr(src1), C1, B, H, W, ksize, _ptr(wgt), _ptr(sc), Csc,
               _ptr(sc1), Csc1, _ptr(sc_wgt), _ptr(bias), None if temb is None else temb.data_ptr() + 4 * temb_off,
               0 if temb is None else temb.shape[1], _ptr(res), 0 if res is None else res.shape[-1], float(out_scale), _ptr(comb),
               _ptr(comb_w), _ptr(comb_b), out.data_ptr(), cout, out.shape[-1], _ptr(stats),
@@ -110,9 +162,8 @@ _VARIANT = {"v": 0}
 
 
 def get_option(name):
-    v = C.c_int(0)
-    _lib.call("snrse_get_option", name.encode(), C.addressof(v))
-    return v.value
+    """A switch or read-back of the calling thread's current context on the current device."""
+    return context().get_option(name)
 
 
 KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 5: "conv_halo5_kernel", 10: "conv_head_kernel"}
@@ -162,8 +213,12 @@ def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):
 STAT_SLOTS = 16  # SNRSE_STAT_SLOTS (include/snrse.h)
 
 
-_ARENA = []  # active StatsArena stack (innermost last)
-_ZEROED = {"v": 0}  # mirror of the library's "stats_zeroed" option
+def _arena_stack():
+    """The calling thread's active StatsArena stack (innermost last)."""
+    st = getattr(_TLS, "arenas", None)
+    if st is None:
+        st = _TLS.arenas = []
+    return st
 
 
 class StatsArena:
@@ -182,11 +237,11 @@ class StatsArena:
         if self.buf is not None:
             self.buf.zero_()
         self.off, self.need = 0, 0
-        _ARENA.append(self)
+        _arena_stack().append(self)
         return self
 
     def __exit__(self, *exc):
-        _ARENA.remove(self)
+        _arena_stack().remove(self)
         if self.buf is None or self.need > self.buf.numel():
             self.buf = torch.empty(self.need, dtype=torch.float64, device=self.device)
         return False
@@ -201,15 +256,14 @@ class StatsArena:
         return t
 
 
-def _stats_zeroed(*bufs):
-    """Set the library's "stats_zeroed" option for a producer writing into `bufs`."""
+def _stats_zeroed(cx, *bufs):
+    """Set context cx's "stats_zeroed" switch for a producer writing into `bufs`."""
     bufs = [b for b in bufs if b is not None]
     if not bufs:
         return
     z = int(all(getattr(b, "_snrse_zeroed", False) for b in bufs))
-    if _ZEROED["v"] != z:
-        _lib.call("snrse_set_option", b"stats_zeroed", z)
-        _ZEROED["v"] = z
+    if cx.zeroed != z:
+        cx.set_option("stats_zeroed", z)
 
 
 def new_stats(x_or_shape, C=None):
@@ -220,8 +274,9 @@ def new_stats(x_or_shape, C=None):
         B, C, dev = x_or_shape.shape[0], x_or_shape.shape[-1], x_or_shape.device
     else:
         B, dev = x_or_shape, torch.device("cuda", torch.cuda.current_device())
-    if _ARENA and _ARENA[-1].device == torch.device(dev):
-        t = _ARENA[-1].take(B * STAT_SLOTS * C * 2)
+    st = _arena_stack()
+    if st and st[-1].device == torch.device(dev):
+        t = st[-1].take(B * STAT_SLOTS * C * 2)
         if t is not None:
             t = t.view(B, STAT_SLOTS, C, 2)
             t._snrse_zeroed = True
@@ -241,8 +296,9 @@ def gn_stats(src0, src1=None):
     C1 = 0 if src1 is None else src1.shape[3]
     s0 = new_stats(src0)
     s1 = None if src1 is None else new_stats(src1)
-    _stats_zeroed(s0, s1)
-    _lib.call("snrse_gn_stats", _ptr(src0), C0, _ptr(src1), C1, B, H * W, s0.data_ptr(), _ptr(s1),
+    cx = context(src0.device)
+    _stats_zeroed(cx, s0, s1)
+    _lib.call("snrse_gn_stats", cx.ptr, _ptr(src0), C0, _ptr(src1), C1, B, H * W, s0.data_ptr(), _ptr(s1),
               code(src0.dtype), _stream())
     return s0, s1
 
@@ -289,7 +345,7 @@ def gn_resample(x, scale=None, shift=None, act=True, mode="down", want_raw=False
     Ho, Wo = (H // 2, W // 2) if m == 1 else (2 * H, 2 * W)
     oa = torch.empty(B, Ho, Wo, C, device=x.device, dtype=x.dtype)
     orw = torch.empty_like(oa) if want_raw else None
-    _lib.call("snrse_gn_resample", x.data_ptr(), C, B, H, W, _ptr(scale), _ptr(shift), int(bool(act)), m,
+    _lib.call("snrse_gn_resample", _cx(x.device), x.data_ptr(), C, B, H, W, _ptr(scale), _ptr(shift), int(bool(act)), m,
               oa.data_ptr(), _ptr(orw), _stream())
     return oa, orw
 
@@ -351,8 +407,9 @@ def input_conv(x, y, wgt, bias):
     h = torch.empty(B, F, T, 128, device=x.device, dtype=torch.bfloat16)
     pyr = torch.empty(B, F, T, 4, device=x.device, dtype=torch.float32)
     st = new_stats(B, 128)
-    _stats_zeroed(st)
-    _lib.call("snrse_input_conv", x.data_ptr(), y.data_ptr(), B, F, T, wgt.data_ptr(), bias.data_ptr(),
+    cx = context(x.device)
+    _stats_zeroed(cx, st)
+    _lib.call("snrse_input_conv", cx.ptr, x.data_ptr(), y.data_ptr(), B, F, T, wgt.data_ptr(), bias.data_ptr(),
               h.data_ptr(), pyr.data_ptr(), st.data_ptr(), _stream())
     return h, st, pyr
 
@@ -477,7 +534,10 @@ def upfirdn2d(inp, kernel, up=1, down=1, pad=(0, 0)):
 
 
 def set_option(name: str, value: int):
+    """Process-wide switch: the library's process default context and every live LaunchContext."""
     _lib.call("snrse_set_option", name.encode(), int(value))
+    for c in list(_CONTEXTS):
+        c.set_option(name, value)
     if name == "conv_variant":
         _VARIANT["v"] = int(value)
 
