@@ -70,6 +70,36 @@ class BBED:
         return float(self.std(self.T))
 
 
+class PROPOSED_1:
+    """sdes.py:314-392: BBED in the (sigma_min, sigma_max) parameterisation, restated as written
+    (diffusion sigma_max * t * sqrt(theta), sdes.py:359-361; std sdes.py:371-378)."""
+
+    def __init__(self, T=0.99, sigma_min=1.0, sigma_max=1.0, theta=0.53, N=30):
+        self.T, self.sigma_min, self.sigma_max, self.theta, self.N = T, sigma_min, sigma_max, theta, N
+        self.logsig = math.log(sigma_max / sigma_min)
+        self.ratio = sigma_max / sigma_min
+        self.Eilog = sc.expi(-2 * self.logsig)
+
+    def g(self, t):
+        return self.sigma_max * t * math.sqrt(self.theta)
+
+    def drift(self, x, t, y):
+        return (y - x) / (1.0 - t)
+
+    def std(self, t):
+        t = np.asarray(t, dtype=np.float64)
+        Eis = sc.expi(2 * (t - 1) * self.logsig) - self.Eilog
+        k = 2 * self.sigma_max ** 2 * self.logsig
+        var = self.sigma_min ** 2 * (self.ratio ** (2 * t) - 1 + t) + k * (1 - t) * Eis
+        return np.sqrt(var * (1 - t) * self.theta)
+
+    def mean(self, x0, t, y):
+        return x0 * (1 - t) + y * t
+
+    def prior_std(self):
+        return float(self.std(self.T))
+
+
 def pc_sample(sde, score_fn, Y, noise, predictor="reverse_diffusion", corrector="ald",
               N=None, eps=0.03, snr=0.5, corrector_steps=1, denoise=True):
     """pc_sampler (sampling/__init__.py:54-75) for a batch Y (complex [B,1,F,T]).

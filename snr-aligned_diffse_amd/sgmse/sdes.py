@@ -1,6 +1,6 @@
-"""SDEs of the enhancement path — reference API (sgmse/sdes.py:20-307).
+"""SDEs of the enhancement path — reference API (sgmse/sdes.py:20-392).
 
-`OUVESDE` and `BBED` keep the reference's method names and shapes (sde, marginal_prob,
+`OUVESDE`, `BBED` and `PROPOSED_1` keep the reference's method names and shapes (sde, marginal_prob,
 _mean, _std, prior_sampling, discretize, reverse, copy, N, T) so user code and the
 samplers interoperate.  The per-element work of the samplers does not go through these
 methods: `spec()` hands the scalar side (float64 host math) to snrse.sampler, whose fused
@@ -203,10 +203,68 @@ class BBED(SDE):
         return SDESpec("bbed", k=self.k, theta=self.theta, T=float(self.T))
 
 
+@SDERegistry.register("proposed_1")
+class PROPOSED_1(SDE):
+    """BBED in the (sigma_min, sigma_max) parameterisation (reference sdes.py:312-392; k = sigma_max /
+    sigma_min).  As written there, the diffusion is sigma_max * t * sqrt(theta) (linear in t, sdes.py:359)
+    while the marginal std uses the exponential form (sdes.py:371-378); both are kept as written."""
+
+    @staticmethod
+    def add_argparse_args(parser):
+        parser.add_argument("--sde-n", type=int, default=1000, help="The number of timesteps in the SDE discretization.")
+        parser.add_argument("--T_sampling", type=float, default=0.99, help="The T so that t < T during sampling in the train step.")
+        parser.add_argument("--sigma-min", type=float, default=1, help="The minimum sigma to use. Set it to 1 and dont change it.")
+        parser.add_argument("--sigma-max", type=float, default=1, help="This is k, the base of diffusion term, when sigma min is 1.")
+        parser.add_argument("--theta", type=float, default=0.53, help="This rescales the diffusion term")
+        return parser
+
+    def __init__(self, T_sampling=0.99, sigma_min=1.0, sigma_max=1.0, theta=0.53, N=1000, **kwargs):
+        super().__init__(N)
+        self.sigma_min, self.sigma_max, self.theta = sigma_min, sigma_max, theta
+        self.logsig = np.log(self.sigma_max / self.sigma_min)
+        self.ratio = self.sigma_max / self.sigma_min
+        self.Eilog = sc.expi(-2 * self.logsig)
+        self.T = T_sampling
+        self.Tc = 1
+
+    def copy(self):
+        return PROPOSED_1(self.T, self.sigma_min, self.sigma_max, self.theta, N=self.N)
+
+    def sde(self, x, t, y):
+        tb = _bc(t, x)
+        drift = (y - x) / (self.Tc - tb)
+        return drift, (self.sigma_max * t) * np.sqrt(self.theta)
+
+    def _mean(self, x0, t, y):
+        time = (t / self.Tc)[:, None, None, None]
+        return x0 * (1 - time) + y * time
+
+    def _std(self, t):
+        t64 = t.detach().cpu().double().numpy()
+        Eis = sc.expi(2 * (t64 - 1) * self.logsig) - self.Eilog
+        k = 2 * self.sigma_max ** 2 * self.logsig
+        var = (self.sigma_min ** 2 * (self.ratio ** (2 * t64) - 1 + t64) + k * (1 - t64) * Eis) * (1 - t64) * self.theta
+        return torch.sqrt(torch.as_tensor(var, device=t.device)).to(t.dtype if t.is_floating_point() else torch.float32)
+
+    def marginal_prob(self, x0, t, y):
+        return self._mean(x0, t, y), self._std(t)
+
+    def prior_sampling(self, shape, y):
+        if shape != y.shape:
+            warnings.warn(f"Target shape {shape} does not match shape of y {y.shape}! Ignoring target shape.")
+        std = self._std(self.T * torch.ones((y.shape[0],), device=y.device))
+        z = torch.randn_like(y)
+        return y + z * std[:, None, None, None], z
+
+    def spec(self):
+        return SDESpec("proposed_1", sigma_min=self.sigma_min, sigma_max=self.sigma_max, theta=self.theta,
+                       T=float(self.T))
+
+
 def sde_spec(sde) -> SDESpec:
     if hasattr(sde, "spec"):
         return sde.spec()
     raise TypeError(f"no scalar spec for SDE {type(sde).__name__}")
 
 
-__all__ = ["SDERegistry", "SDE", "OUVESDE", "BBED", "math"]
+__all__ = ["SDERegistry", "SDE", "OUVESDE", "BBED", "PROPOSED_1", "math"]

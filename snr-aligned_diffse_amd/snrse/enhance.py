@@ -97,7 +97,7 @@ class PCEnhancer:
                     return e.value
         cur = torch.cuda.current_stream(Y.device)
         bounds = [(B * h // nl, B * (h + 1) // nl) for h in range(nl)]
-        lanes = []
+        lanes, lane_noise = [], []
         for h, (a, b) in enumerate(bounds):
             s = self._lane_streams.get((Y.device, h))
             if s is None:
@@ -105,7 +105,8 @@ class PCEnhancer:
             s.wait_stream(cur)
             with torch.cuda.stream(s):
                 Yh = Y[a:b].contiguous()
-                lanes.append((s, self._iter(Yh, sampler.LaneNoise(noise, a, b, B))))
+                lane_noise.append(sampler.LaneNoise(noise, a, b, B))
+                lanes.append((s, self._iter(Yh, lane_noise[-1])))
         starts = None
         if self.stagger:
             # lane k's first launch waits for lane k-1's first evaluation to pass the bottleneck
@@ -123,6 +124,7 @@ class PCEnhancer:
             starts = start
         res = sampler.pc_sample_lockstep(lanes, on_first=starts)
         self.net.mid_hook = None
+        noise.i = lane_noise[0].i  # the parent has now supplied the lanes' draws (as the one-stream run does)
         for (s, _), (x, _) in zip(lanes, res):
             cur.wait_stream(s)
             x.record_stream(cur)

@@ -11,7 +11,7 @@ Step algebra (all elementwise on complex64, per-utterance scalars a, by, c, s):
   ALD corrector (correctors.py:69-81):   a=1, by=0, c=e, s=sqrt(2e), e = 2 (snr std(t))^2
   reverse diffusion (predictors.py:75-80 with SDE.discretize sdes.py:86-91, RSDE 132-140):
       OUVE drift theta (y - x):  a = 1 + theta dt, by = -theta dt, c = G^2, s = G
-      BBED drift (y - x)/(1 - t): a = 1 + dt/(1-t), by = -dt/(1-t), c = G^2, s = G
+      BBED / PROPOSED_1 drift (y - x)/(1 - t): a = 1 + dt/(1-t), by = -dt/(1-t), c = G^2, s = G
       with G = g(t) sqrt(dt), dt = stepsize
   Euler-Maruyama (predictors.py:46-52): dt = -1/N,
       a = 1 - theta dt (OUVE) | 1 - dt/(1-t) (BBED), by = -(a - 1), c = -g^2 dt, s = g sqrt(-dt)
@@ -45,21 +45,37 @@ class SDESpec:
             self.logk = math.log(self.k)
             self.Eilog = float(sc.expi(-2 * self.logk))
             self.T = float(kw.get("T", 0.999))
+        elif kind == "proposed_1":
+            # BBED in the (sigma_min, sigma_max) parameterisation, sdes.py:314-392
+            self.sigma_min = float(kw.get("sigma_min", 1.0))
+            self.sigma_max = float(kw.get("sigma_max", 1.0))
+            self.theta = float(kw.get("theta", 0.53))
+            self.logsig = math.log(self.sigma_max / self.sigma_min)
+            self.ratio = self.sigma_max / self.sigma_min
+            self.Eilog = float(sc.expi(-2 * self.logsig))
+            self.T = float(kw.get("T", 0.99))
         else:
             raise ValueError(f"SDE kind {kind} unknown")
 
     def g(self, t):
         if self.kind == "ouve":
             return self.sigma_min * (self.sigma_max / self.sigma_min) ** t * math.sqrt(2 * self.logsig)
+        if self.kind == "proposed_1":  # sdes.py:359-361: sigma = sigma_max * t (linear in t, as written)
+            return self.sigma_max * t * math.sqrt(self.theta)
         return self.k ** t * math.sqrt(self.theta)
 
     def std(self, t):
         if self.kind == "ouve":
             a = self.sigma_min ** 2 * math.exp(-2 * self.theta * t) * (math.exp(2 * (self.theta + self.logsig) * t) - 1)
             return math.sqrt(a * self.logsig / (self.theta + self.logsig))
-        Eis = float(sc.expi(2 * (t - 1) * self.logk)) - self.Eilog
-        h = 2 * self.k ** 2 * self.logk
-        var = (self.k ** (2 * t) - 1 + t) + h * (1 - t) * Eis
+        if self.kind == "proposed_1":  # sdes.py:371-378
+            Eis = float(sc.expi(2 * (t - 1) * self.logsig)) - self.Eilog
+            k = 2 * self.sigma_max ** 2 * self.logsig
+            var = self.sigma_min ** 2 * (self.ratio ** (2 * t) - 1 + t) + k * (1 - t) * Eis
+        else:
+            Eis = float(sc.expi(2 * (t - 1) * self.logk)) - self.Eilog
+            h = 2 * self.k ** 2 * self.logk
+            var = (self.k ** (2 * t) - 1 + t) + h * (1 - t) * Eis
         v = var * (1 - t) * self.theta
         return math.sqrt(v) if v >= 0 else float("nan")
 
@@ -130,6 +146,7 @@ class LaneNoise(NoiseSource):
     def __init__(self, parent: NoiseSource, a, b, rows):
         super().__init__(parent.seed, None)
         self.parent_tape, self.a, self.b, self.rows = parent.tape, a, b, rows
+        self.i = parent.i  # continue where the parent's earlier draws left off
 
     def next(self, numel):
         i = self.i

@@ -539,24 +539,26 @@ def consistency_loss(net, X, Y, n, z, sigma_max, loss_type="mse", fixed_snr=None
 # ----------------------------------------------------------------------------- optimizer
 class FusedAdam(torch.optim.Optimizer):
     """torch.optim.Adam (betas, eps; no weight decay, amsgrad or maximize) whose step runs as ONE HIP
-    launch over every parameter tensor that has a gradient (snrse_adam_ema; torch skips the others too);
+    launch over every parameter tensor that has a gradient (snrse_adam_ema; torch skips the others too),
+    one launch per distinct per-tensor step count (torch's bias correction uses each tensor's own);
     `ema` (a sgmse.ema.EMAState) is updated in the same launch with torch_ema 0.3's rule,
-    decay = min(decay, (1 + n) / (10 + n)), its shadows created from the parameters on first use."""
+    decay = min(decay, (1 + n) / (10 + n)), its shadows created from the parameters on first use; shadows of
+    parameters without a gradient move too (torch_ema updates every requires_grad shadow)."""
 
     def __init__(self, params, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, ema=None):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
         self.ema = ema
-        self._key = None
+        self._chunk_cache = {}
 
     def _chunks(self, ps):
+        """(tensor index, start) of every 2048-element chunk of the tensors `ps`, on the device."""
         tix, starts = [], []
         for i, p in enumerate(ps):
             for s0 in range(0, p.numel(), 2048):
                 tix.append(i)
                 starts.append(s0)
         dev = ps[0].device
-        self._tix = torch.tensor(tix, dtype=torch.int32, device=dev)
-        self._starts = torch.tensor(starts, dtype=torch.int64, device=dev)
+        return (torch.tensor(tix, dtype=torch.int32, device=dev), torch.tensor(starts, dtype=torch.int64, device=dev))
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -574,6 +576,7 @@ class FusedAdam(torch.optim.Optimizer):
             n_up = (0 if self.ema.num_updates is None else self.ema.num_updates) + 1
             self.ema.num_updates = n_up
             decay = min(self.ema.decay, (1 + n_up) / (10 + n_up))
+        updated = set()
         for group in self.param_groups:
             ps = [p for p in group["params"] if p.grad is not None]
             if not ps:
@@ -587,23 +590,39 @@ class FusedAdam(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 st["step"] += 1
-            key = tuple(id(p) for p in ps)
-            if key != self._key:
-                self._chunks(ps)
-                self._key = key
-            rec = np.zeros((len(ps), 6), dtype=np.int64)
-            for i, p in enumerate(ps):
-                st = self.state[p]
-                sh = shadow_of.get(id(p))
-                rec[i] = [p.data_ptr(), p.grad.contiguous().data_ptr(), st["exp_avg"].data_ptr(),
-                          st["exp_avg_sq"].data_ptr(), 0 if sh is None else sh.data_ptr(), p.numel()]
-            table = torch.from_numpy(rec).to(ps[0].device)
-            step = int(self.state[ps[0]]["step"])
-            b1, b2 = group["betas"]
-            _call("snrse_adam_ema", table.data_ptr(), self._tix.data_ptr(), self._starts.data_ptr(),
-                  int(self._tix.numel()), float(group["lr"]), float(b1), float(b2), float(group["eps"]),
-                  float(1 - b1 ** step), float(math.sqrt(1 - b2 ** step)), float(decay))
-            self._keep = table  # the launch reads it asynchronously
+            # torch.optim.Adam corrects every tensor with its own step count: one launch per distinct count
+            # (a single one while every parameter gets a gradient on every step)
+            by_step = {}
+            for p in ps:
+                by_step.setdefault(int(self.state[p]["step"]), []).append(p)
+            keep = []
+            for step, sub in by_step.items():
+                key = tuple(id(p) for p in sub)
+                if key not in self._chunk_cache:
+                    self._chunk_cache[key] = self._chunks(sub)
+                tix, starts = self._chunk_cache[key]
+                rec = np.zeros((len(sub), 6), dtype=np.int64)
+                for i, p in enumerate(sub):
+                    st = self.state[p]
+                    sh = shadow_of.get(id(p))
+                    g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                    keep.append(g)  # a temporary copy must outlive the asynchronous launch
+                    rec[i] = [p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
+                              st["exp_avg_sq"].data_ptr(), 0 if sh is None else sh.data_ptr(), p.numel()]
+                table = torch.from_numpy(rec).to(sub[0].device)
+                keep.append(table)  # the launch reads it asynchronously
+                b1, b2 = group["betas"]
+                _call("snrse_adam_ema", table.data_ptr(), tix.data_ptr(), starts.data_ptr(),
+                      int(tix.numel()), float(group["lr"]), float(b1), float(b2), float(group["eps"]),
+                      float(1 - b1 ** step), float(math.sqrt(1 - b2 ** step)), float(decay))
+            self._keep = keep
+            updated.update(id(p) for p in ps)
+        if self.ema is not None:
+            # torch_ema 0.3 moves EVERY requires_grad shadow on every update, gradient or not:
+            # s = decay s + (1 - decay) p for the parameters the fused launch did not touch
+            for p, sh in zip(eps_, self.ema.shadow_params):
+                if id(p) not in updated and p.requires_grad:
+                    _call("snrse_axpby", p.data_ptr(), sh.data_ptr(), p.numel(), float(1 - decay), float(decay))
         return loss
 
 

@@ -36,19 +36,20 @@ def test_registries():
     from sgmse.sdes import SDERegistry
     assert set(PredictorRegistry.get_all_names()) >= {"reverse_diffusion", "euler_maruyama", "none"}
     assert set(CorrectorRegistry.get_all_names()) >= {"ald", "langevin", "none"}
-    assert set(SDERegistry.get_all_names()) >= {"ouve", "bbed"}
+    assert set(SDERegistry.get_all_names()) >= {"ouve", "bbed", "proposed_1"}
     with pytest.raises(ValueError, match="unknown"):
         PredictorRegistry.get_by_name("nope")
 
 
 def test_sde_api_matches_golden():
-    from sgmse.sdes import BBED, OUVESDE
+    from sgmse.sdes import BBED, OUVESDE, PROPOSED_1, SDERegistry
     g = golden("sde.npz")
     ts = torch.tensor(g["t"])
     x = torch.from_numpy(fnormal("golden.sde.x", (5, 1, 4, 4), complex_=True))
     y = torch.from_numpy(fnormal("golden.sde.y", (5, 1, 4, 4), complex_=True))
     for nm, s in (("ouve", OUVESDE(1.5, 0.05, 0.5, N=30)), ("ouve_smax1", OUVESDE(1.5, 0.05, 1.0, N=30)),
-                  ("bbed", BBED(0.999, 2.6, 0.52, N=30))):
+                  ("bbed", BBED(0.999, 2.6, 0.52, N=30)), ("proposed_1", PROPOSED_1(0.99, 1.0, 2.6, 0.52, N=30)),
+                  ("proposed_1b", SDERegistry.get_by_name("proposed_1")(0.99, 0.5, 3.0, 0.53, N=30))):
         np.testing.assert_allclose(s._std(ts).double().numpy(), g[f"{nm}_std"], rtol=2e-6)
         d, gg = s.sde(x, ts[:, None, None, None], y)
         np.testing.assert_allclose(d.numpy(), g[f"{nm}_drift"], rtol=2e-5, atol=1e-5)

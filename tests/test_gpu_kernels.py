@@ -311,7 +311,8 @@ def test_pc_variants_generic(gpu):
 
     for key in [k for k in g.files if "__" in k and not k.endswith(("__ns", "__draws"))]:
         sde_name, pred, corr = key.split("__")
-        sde = sampler.SDESpec("ouve") if sde_name == "ouve" else sampler.SDESpec("bbed")
+        sde = {"ouve": sampler.SDESpec("ouve"), "bbed": sampler.SDESpec("bbed"),
+               "proposed_1": sampler.SDESpec("proposed_1", sigma_min=1.0, sigma_max=2.6, theta=0.52)}[sde_name]
         Yc = Y if sde_name == "ouve" else Y[:1].contiguous()
         tape = Tape(f"golden.pcv.{sde_name}.{pred}.{corr}", gpu)
         shape = (Yc.shape[0], 1) + tuple(Yc.shape[1:])

@@ -1,7 +1,7 @@
 """GPU parity of the consistency-training step against the reference.
 
 tests/golden/train_step.npz holds the loss of ScoreModel._step (sebridge_v3, snr_conditioned='true',
-model.py:361-390) and the parameter gradients of loss.backward(), computed by tools/gen_golden.py
+model.py:361-390, and 'fixed', model.py:293-326) and the parameter gradients of loss.backward(), computed by tools/gen_golden.py
 with the REFERENCE NCSNpp module and torch autograd on the CPU (formula weights, B=2 x 256 x 64,
 n = (3, 17), formula noise).  Here the same batch runs through sgmse.model.ScoreModel._step on the
 HIP kernels (forward, backward and loss all HIP, snrse/train.py).
@@ -30,9 +30,9 @@ pytestmark = pytest.mark.gpu
 REPORT_DIR = os.environ.get("SNRSE_REPORT_DIR", os.path.join(ROOT, "gpurun_out"))
 
 
-def _model(loss_type):
+def _model(loss_type, snr_conditioned="true"):
     from sgmse.model import ScoreModel
-    hp = dict(backbone="ncsnpp", sde="ouve", model_type="sebridge_v3", snr_conditioned="true", theta=1.5,
+    hp = dict(backbone="ncsnpp", sde="ouve", model_type="sebridge_v3", snr_conditioned=snr_conditioned, theta=1.5,
               sigma_min=0.05, sigma_max=0.5, N=30, compute_dtype="fp32", fixed_snr=0.17783, loss_type=loss_type)
     m = ScoreModel(**hp)
     m.dnn.load_state_dict({k: torch.from_numpy(v) for k, v in formula_sd("ncsnpp").items()})
@@ -48,14 +48,20 @@ def _batch(gpu):
     return g, x.to(gpu), y.to(gpu), z.to(gpu)
 
 
+@pytest.mark.parametrize("snr_conditioned", ["true", "fixed"])
 @pytest.mark.parametrize("loss_type", ["mse", "sqrt_mse"])
-def test_consistency_step_loss_and_grads_vs_reference(gpu, loss_type):
+def test_consistency_step_loss_and_grads_vs_reference(gpu, loss_type, snr_conditioned):
+    """'true': model.py:361-390; 'fixed': model.py:293-326 (mu_t = H(x_ori + (H^-1(y) - x_ori) fixed_snr t),
+    golden keys prefixed fixed_, fixed_snr 0.17783)."""
     g, x, y, z = _batch(gpu)
-    m = _model(loss_type)
+    m = _model(loss_type, snr_conditioned)
+    if snr_conditioned == "fixed":
+        assert abs(float(g["fixed_snr"]) - m.fixed_snr) < 1e-12
+    key = loss_type if snr_conditioned == "true" else f"fixed_{loss_type}"
     loss = m._step((x, y), 0, n=g["n"], noise=z)
     loss.backward()
     torch.cuda.synchronize()
-    ref_loss = float(g[f"{loss_type}_loss"])
+    ref_loss = float(g[f"{key}_loss"])
     err_loss = abs(float(loss) - ref_loss) / abs(ref_loss)
     params = dict(m.dnn.named_parameters())
     names = [str(k) for k in g["names"]]
@@ -68,9 +74,9 @@ def test_consistency_step_loss_and_grads_vs_reference(gpu, loss_type):
         got_head.append(gd.reshape(-1)[:head].numpy())
         got_sq.append(float((gd ** 2).sum()))
     got_head = np.concatenate(got_head)
-    ref_head = g[f"{loss_type}_head"].astype(np.float64)
+    ref_head = g[f"{key}_head"].astype(np.float64)
     rel_head = float(np.sqrt(np.mean((got_head - ref_head) ** 2)) / np.sqrt(np.mean(ref_head ** 2)))
-    ref_sq = g[f"{loss_type}_gsq"]
+    ref_sq = g[f"{key}_gsq"]
     rel_sq = np.abs(np.asarray(got_sq) - ref_sq) / np.maximum(ref_sq, 1e-30)
     key_bias = {}
     for i, k in enumerate(names):
@@ -80,13 +86,13 @@ def test_consistency_step_loss_and_grads_vs_reference(gpu, loss_type):
             rel_sq[i] = 0.0
     full = {}
     for k in [str(s) for s in g["full_keys"]]:
-        r = g[f"{loss_type}_full__{k}"].astype(np.float64)
+        r = g[f"{key}_full__{k}"].astype(np.float64)
         a = params[k.replace("dnn.", "")].grad.detach().double().cpu().numpy()
         full[k] = float(np.sqrt(np.mean((a - r) ** 2)) / (np.sqrt(np.mean(r ** 2)) + 1e-30))
     order = np.argsort(-rel_sq)[:5]
     worst = [(names[i], float(rel_sq[i])) for i in order]
     os.makedirs(REPORT_DIR, exist_ok=True)
-    with open(os.path.join(REPORT_DIR, f"train_step_{loss_type}_vs_reference.json"), "w") as f:
+    with open(os.path.join(REPORT_DIR, f"train_step_{key}_vs_reference.json"), "w") as f:
         json.dump({"loss": float(loss), "ref_loss": ref_loss, "rel_err_loss": err_loss,
                    "rel_rms_grad_heads": rel_head, "max_rel_err_grad_sumsq": float(rel_sq.max()),
                    "worst_sumsq": worst, "rel_rms_full_tensors": full,
@@ -129,6 +135,47 @@ def test_fused_adam_and_ema_match_torch(gpu):
     for s, r in zip(ema.shadow_params, shadow):
         assert torch.allclose(s, r, rtol=1e-6, atol=1e-6)
     assert ema.num_updates == 3
+
+
+def test_fused_adam_missing_and_noncontiguous_grads_match_torch(gpu):
+    """Per-tensor step counts (a parameter without a gradient on step 2 falls one step behind, as in
+    torch.optim.Adam), EMA shadows of parameters without a gradient still move (torch_ema 0.3 updates
+    every requires_grad shadow), and a non-contiguous gradient is read correctly (its contiguous copy
+    stays alive until the asynchronous launch has run)."""
+    from sgmse.ema import EMAState
+    from snrse.train import FusedAdam
+    gen = torch.Generator(device=gpu).manual_seed(4)
+    mod = torch.nn.Module()
+    shapes = [(64, 32), (33,), (4097,)]
+    mod.ps = torch.nn.ParameterList([torch.nn.Parameter(torch.randn(s, device=gpu, generator=gen)) for s in shapes])
+    ref = [p.detach().clone().requires_grad_(True) for p in mod.ps]
+    ema = EMAState(mod, 0.999)
+    opt = FusedAdam(mod.parameters(), lr=1e-3, ema=ema)
+    topt = torch.optim.Adam(ref, lr=1e-3)
+    shadow = [p.detach().clone() for p in ref]
+    for it in range(4):
+        grads = [torch.randn(s, device=gpu, generator=gen) for s in shapes]
+        for k, (p, q, gr) in enumerate(zip(mod.ps, ref, grads)):
+            if it == 1 and k == 1:  # no gradient for parameter 1 on step 2
+                p.grad, q.grad = None, None
+                continue
+            if k == 0:  # a non-contiguous (transposed-view) gradient
+                p.grad = gr.t().contiguous().t()
+                assert not p.grad.is_contiguous()
+            else:
+                p.grad = gr.clone()
+            q.grad = gr.clone()
+        opt.step()
+        topt.step()
+        decay = min(0.999, (1 + it + 1) / (10 + it + 1))
+        with torch.no_grad():
+            for s, q in zip(shadow, ref):
+                s.sub_((1.0 - decay) * (s - q))
+    torch.cuda.synchronize()
+    for p, q in zip(mod.ps, ref):
+        assert torch.allclose(p, q, rtol=1e-6, atol=1e-6), (p - q).abs().max()
+    for s, r in zip(ema.shadow_params, shadow):
+        assert torch.allclose(s, r, rtol=1e-6, atol=1e-6), (s - r).abs().max()
 
 
 def test_training_loop_runs_and_updates(gpu):

@@ -84,7 +84,8 @@ def test_sde_tables():
     x = fnormal("golden.sde.x", (5, 1, 4, 4), complex_=True)
     y = fnormal("golden.sde.y", (5, 1, 4, 4), complex_=True)
     sdes = {"ouve": sde_ref.OUVE(1.5, 0.05, 0.5), "ouve_smax1": sde_ref.OUVE(1.5, 0.05, 1.0),
-            "bbed": sde_ref.BBED(0.999, 2.6, 0.52)}
+            "bbed": sde_ref.BBED(0.999, 2.6, 0.52), "proposed_1": sde_ref.PROPOSED_1(0.99, 1.0, 2.6, 0.52),
+            "proposed_1b": sde_ref.PROPOSED_1(0.99, 0.5, 3.0, 0.53)}
     for nm, s in sdes.items():
         np.testing.assert_allclose(s.std(ts), g[f"{nm}_std"], rtol=2e-6)
         np.testing.assert_allclose([s.g(t) for t in ts], g[f"{nm}_g"], rtol=2e-6)
@@ -98,6 +99,8 @@ def test_sde_tables():
     assert math.isnan(float(bb.std(1.0)))
     np.testing.assert_allclose(sdes["ouve"].std(1.0), 0.388983, atol=2e-6)
     np.testing.assert_allclose(sdes["ouve_smax1"].std(1.0), 0.816252, atol=2e-6)
+    # PROPOSED_1 with sigma_min = 1, sigma_max = k is BBED's marginal std (sdes.py:312-329)
+    np.testing.assert_allclose(sdes["proposed_1"].std(ts), bb.std(ts), rtol=1e-12)
 
 
 class Tape:
@@ -119,8 +122,9 @@ def test_pc_variants():
 
     for key in [k for k in g.files if "__" in k and not k.endswith(("__ns", "__draws"))]:
         sde_name, pred, corr = key.split("__")
-        sde = sde_ref.OUVE(1.5, 0.05, 0.5, N=6) if sde_name == "ouve" else sde_ref.BBED(0.999, 2.6, 0.52, N=6)
-        # the reference promotes BBED runs to complex128 (sdes.py:292,303)
+        sde = {"ouve": lambda: sde_ref.OUVE(1.5, 0.05, 0.5, N=6), "bbed": lambda: sde_ref.BBED(0.999, 2.6, 0.52, N=6),
+               "proposed_1": lambda: sde_ref.PROPOSED_1(0.99, 1.0, 2.6, 0.52, N=6)}[sde_name]()
+        # the reference promotes BBED / PROPOSED_1 runs to complex128 (sdes.py:292,303, 376,388)
         Yc = Y if sde_name == "ouve" else Y[:1].to(torch.complex128)
         tape = Tape(f"golden.pcv.{sde_name}.{pred}.{corr}", Yc.dtype)
         xr, ns = sde_ref.pc_sample(sde, score_fn, Yc, tape, predictor=pred, corrector=corr)

@@ -9,7 +9,7 @@ the GPU box).  The reference's own torch modules produce every expected output h
                                              GaussianFourierProjection 32-43)
   sgmse.backbones.ncsnpp_utils.up_or_down_sampling (upsample_2d/downsample_2d 195-257)
   sgmse.backbones.snrnet.SNRNet             (snrnet.py:47-97)
-  sgmse.sdes.{OUVESDE,BBED}                 (sdes.py:149-307)
+  sgmse.sdes.{OUVESDE,BBED,PROPOSED_1}      (sdes.py:149-392)
   sgmse.sampling.get_pc_sampler             (sampling/__init__.py:28-80)
 
 Import recipe: stub torch.utils.cpp_extension.load before importing, so
@@ -158,10 +158,12 @@ def gen_sde():
     ou = ref_sdes.OUVESDE(theta=1.5, sigma_min=0.05, sigma_max=0.5, N=30)
     ou1 = ref_sdes.OUVESDE(theta=1.5, sigma_min=0.05, sigma_max=1.0, N=30)
     bb = ref_sdes.BBED(T_sampling=0.999, k=2.6, theta=0.52, N=30)
+    p1 = ref_sdes.PROPOSED_1(T_sampling=0.99, sigma_min=1.0, sigma_max=2.6, theta=0.52, N=30)
+    p1b = ref_sdes.PROPOSED_1(T_sampling=0.99, sigma_min=0.5, sigma_max=3.0, theta=0.53, N=30)
     x = fnormal("golden.sde.x", (5, 1, 4, 4), complex_=True)
     y = fnormal("golden.sde.y", (5, 1, 4, 4), complex_=True)
     out = {"t": t2n(ts)}
-    for nm, s in (("ouve", ou), ("ouve_smax1", ou1), ("bbed", bb)):
+    for nm, s in (("ouve", ou), ("ouve_smax1", ou1), ("bbed", bb), ("proposed_1", p1), ("proposed_1b", p1b)):
         d, g = s.sde(x, ts[:, None, None, None], y)
         out[f"{nm}_drift"] = t2n(d)
         out[f"{nm}_g"] = t2n(torch.as_tensor(g)).reshape(-1)
@@ -222,13 +224,16 @@ def gen_pc_variants():
     # (sampling/__init__.py:72, predictors.py:46-49, sdes.py:192).
     cases = [("ouve", "reverse_diffusion", "ald"), ("ouve", "reverse_diffusion", "langevin"),
              ("ouve", "reverse_diffusion", "none"), ("ouve", "none", "ald"),
-             ("bbed", "reverse_diffusion", "ald")]
+             ("bbed", "reverse_diffusion", "ald"), ("proposed_1", "reverse_diffusion", "ald")]
     for sde_name, pred, corr in cases:
         if sde_name == "ouve":
             sde = ref_sdes.OUVESDE(theta=1.5, sigma_min=0.05, sigma_max=0.5, N=6)
             Yc = Y
-        else:  # BBED works only for B=1 in the reference (sdes.py:276), see DESIGN.md
+        elif sde_name == "bbed":  # BBED works only for B=1 in the reference (sdes.py:276), see DESIGN.md
             sde = ref_sdes.BBED(T_sampling=0.999, k=2.6, theta=0.52, N=6)
+            Yc = Y[:1]
+        else:  # PROPOSED_1: the same (y - x)/(Tc - t) drift without the [B] reshape (sdes.py:357): B=1 as well
+            sde = ref_sdes.PROPOSED_1(T_sampling=0.99, sigma_min=1.0, sigma_max=2.6, theta=0.52, N=6)
             Yc = Y[:1]
         sampler = ref_sampling.get_pc_sampler(pred, corr, sde=sde, score_fn=score_fn, Y=Yc,
                                               eps=0.03, snr=0.5, corrector_steps=1)
@@ -408,11 +413,13 @@ TRAIN_FULL = ["output_layer.weight", "output_layer.bias", "all_modules.1.bias", 
               "all_modules.21.GroupNorm_0.weight", "all_modules.33.NIN_3.b", "all_modules.75.weight",
               "all_modules.76.weight", "all_modules.76.bias", "all_modules.74.Conv_2.bias"]
 TRAIN_HEAD = 96            # leading elements kept of every other gradient tensor
+TRAIN_FIXED_SNR = 0.17783  # fixed_snr of the 'fixed' branch (the C4 configuration's value)
 
 
 def gen_train_step():
-    """the consistency-training loss of ScoreModel._step, sebridge_v3 +
-    snr_conditioned='true' (model.py:361-390, preconditioned forward 536-541), restated around the
+    """the consistency-training loss of ScoreModel._step, sebridge_v3 with
+    snr_conditioned='true' (model.py:361-390) and 'fixed' (model.py:293-326; keys prefixed fixed_), both
+    with the preconditioned forward of model.py:521-541, restated around the
     REFERENCE NCSNpp module (formula weights) and differentiated by torch autograd on the CPU.  Both loss
     types; the loss, every gradient's (sum, sum of squares, max |g|), the full gradient of a few tensors and
     the first TRAIN_HEAD elements of every other one are stored."""
@@ -427,10 +434,12 @@ def gen_train_step():
     t_n = (eps ** (1 / roh) + ((n - 1) / (N - 1)) * (Tt ** (1 / roh) - eps ** (1 / roh))) ** roh
     t_n1 = (eps ** (1 / roh) + ((n) / (N - 1)) * (Tt ** (1 / roh) - eps ** (1 / roh))) ** roh
     zz = z * sigma_max
-    mu_t_n = spec_fwd_ref(spec_back_ref(x) * (1 - t_n) + spec_back_ref(y) * t_n)
-    mu_t_n1 = spec_fwd_ref(spec_back_ref(x) * (1 - t_n1) + spec_back_ref(y) * t_n1)
-    x_t_n = mu_t_n + t_n * zz
-    x_t_n1 = mu_t_n1 + t_n1 * zz
+    # snr_conditioned 'true' (model.py:372-376): mu_t = H(H^-1(x)(1 - t) + H^-1(y) t)
+    mus_true = [spec_fwd_ref(spec_back_ref(x) * (1 - tt) + spec_back_ref(y) * tt) for tt in (t_n, t_n1)]
+    # snr_conditioned 'fixed' (model.py:304-312): mu_t = H(x_ori + (H^-1(y) - x_ori) fixed_snr t)
+    x_ori = spec_back_ref(x)
+    y0_snr = (spec_back_ref(y) - x_ori) * TRAIN_FIXED_SNR
+    mus_fixed = [spec_fwd_ref(x_ori + y0_snr * tt) for tt in (t_n, t_n1)]
 
     def forward(xx, t, yy):  # ScoreModel.forward, snr_conditioned 'true', sebridge_v3 (model.py:536-541)
         e_, sd = 0.001, 0.5
@@ -439,10 +448,15 @@ def gen_train_step():
         return c_skip * xx + c_out * net(torch.cat([xx, yy], dim=1), t.squeeze(3).squeeze(2).squeeze(1))
 
     out = {"n": np.asarray(TRAIN_N), "t_n": t2n(t_n).reshape(-1), "t_n1": t2n(t_n1).reshape(-1),
+           "fixed_snr": np.float64(TRAIN_FIXED_SNR),
            "full_keys": np.asarray(TRAIN_FULL), "head": np.int64(TRAIN_HEAD)}
     names = [k for k, p in net.named_parameters() if p.requires_grad]
     out["names"] = np.asarray(names)
-    for lt in ("mse", "sqrt_mse"):
+    for branch, lt in (("true", "mse"), ("true", "sqrt_mse"), ("fixed", "mse"), ("fixed", "sqrt_mse")):
+        mu_t_n, mu_t_n1 = mus_true if branch == "true" else mus_fixed
+        x_t_n = mu_t_n + t_n * zz
+        x_t_n1 = mu_t_n1 + t_n1 * zz
+        lt_key = lt if branch == "true" else f"fixed_{lt}"
         net.zero_grad()
         f_theta = forward(x_t_n1, t_n1, mu_t_n1)
         f_theta_minus = forward(x_t_n, t_n, mu_t_n)
@@ -456,13 +470,13 @@ def gen_train_step():
         loss.backward()
         params = dict(net.named_parameters())
         g = {k: params[k].grad.detach().double() for k in names}
-        out[f"{lt}_loss"] = np.float64(loss.item())
-        out[f"{lt}_gsum"] = np.asarray([float(g[k].sum()) for k in names])
-        out[f"{lt}_gsq"] = np.asarray([float((g[k] ** 2).sum()) for k in names])
-        out[f"{lt}_gmax"] = np.asarray([float(g[k].abs().max()) for k in names])
+        out[f"{lt_key}_loss"] = np.float64(loss.item())
+        out[f"{lt_key}_gsum"] = np.asarray([float(g[k].sum()) for k in names])
+        out[f"{lt_key}_gsq"] = np.asarray([float((g[k] ** 2).sum()) for k in names])
+        out[f"{lt_key}_gmax"] = np.asarray([float(g[k].abs().max()) for k in names])
         for k in TRAIN_FULL:
-            out[f"{lt}_full__{k}"] = t2n(g[k].float())
-        out[f"{lt}_head"] = np.concatenate([t2n(g[k].float()).reshape(-1)[:TRAIN_HEAD] for k in names])
+            out[f"{lt_key}_full__{k}"] = t2n(g[k].float())
+        out[f"{lt_key}_head"] = np.concatenate([t2n(g[k].float()).reshape(-1)[:TRAIN_HEAD] for k in names])
     save("train_step.npz", **out)
 
 
