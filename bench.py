@@ -293,11 +293,16 @@ def conv_flops(src0, src1, ksize, cout, sc, sc1):
 
 
 class ConvProbe:
-    """HIP events on the launch stream around every big conv launch during one extra enhance() pass
-    after the timed region (bf16: the halo-path 3x3 convs, ops.halo_ok; fp32 parity mode: every 3x3
-    conv with Cout >= 64), grouped by the kernel that ran (snrse_get_option "last_kernel").
-    achieved = algorithmic FLOPs of the dominant kernel's launches / their summed event time, i.e. mean
-    FLOPs per launch / mean launch duration (the quantity rocprofv3 --stats reports as AverageNs)."""
+    """HIP events on the launch stream around every conv call during one extra enhance() pass after the
+    timed region, recorded by the library itself around the call's kernel launches (snrse_ctx_probe_begin:
+    events without the system-scope fence, so no cache write-back sits inside a bracket -- torch.cuda.Event
+    pairs read ~7 % long on the fp32 path, profiles/r03g_c5_probe_vs_rocprof.json).  The big convs (bf16:
+    the halo-path 3x3 convs, ops.halo_ok; fp32 parity mode: every 3x3 conv with Cout >= 64) are grouped by
+    the kernel that ran.  achieved = algorithmic FLOPs of the dominant kernel's launches / their summed
+    event time, i.e. mean FLOPs per launch / mean launch duration (what rocprofv3 --stats reports as
+    AverageNs; a split-K call's bracket also holds its conv_splitk_finalize)."""
+
+    CAP = 4096
 
     def __init__(self):
         self.rec = []
@@ -308,30 +313,32 @@ class ConvProbe:
 
         def wrapped(src0, wgt, ksize, cout, *a, **kw):
             big = ops.halo_ok(src0, ksize, cout) or (src0.dtype == torch.float32 and ksize == 3 and cout >= 64)
-            if not big:
-                return orig(src0, wgt, ksize, cout, *a, **kw)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            out = orig(src0, wgt, ksize, cout, *a, **kw)
-            e1.record()
-            probe.rec.append((conv_flops(src0, kw.get("src1"), ksize, cout, kw.get("sc"), kw.get("sc1")), e0, e1,
-                              ops.kernel_name(ops.get_option("last_kernel"))))
-            return out
+            probe.rec.append(conv_flops(src0, kw.get("src1"), ksize, cout, kw.get("sc"), kw.get("sc1")) if big else None)
+            return orig(src0, wgt, ksize, cout, *a, **kw)
 
         ops.conv2d = wrapped
         self.orig, self.ops = orig, ops
+        ops.probe_begin(self.CAP)
 
     def uninstall(self):
         self.ops.conv2d = self.orig
 
     def summary(self):
         """{kernel: [flops, ms, launches]} over the probed pass."""
-        torch.cuda.synchronize()
+        ms, kern = self.ops.probe_read(self.CAP)
+        self.ops.probe_begin(0)
+        if len(ms) != min(len(self.rec), self.CAP):
+            raise RuntimeError(f"probe: {len(ms)} timed calls for {len(self.rec)} conv2d calls")
+        if os.environ.get("SNRSE_PROBE_DUMP"):  # per-call record for tools/probe_reconcile.py
+            with open(os.environ["SNRSE_PROBE_DUMP"], "w") as f:
+                json.dump({"ms": ms, "kernel": kern, "flops": self.rec[:len(ms)]}, f)
         by = {}
-        for fl, e0, e1, k in self.rec:
-            d = by.setdefault(k, [0.0, 0.0, 0])
+        for fl, t, k in zip(self.rec, ms, kern):
+            if fl is None:
+                continue
+            d = by.setdefault(self.ops.kernel_name(k), [0.0, 0.0, 0])
             d[0] += fl
-            d[1] += e0.elapsed_time(e1)
+            d[1] += t
             d[2] += 1
         return by
 
@@ -501,6 +508,9 @@ def run(args):
         r = paritycheck.pc_vs_golden(dev, net)
         parity = {k: r[k] for k in ("check", "dtype", "rel_rms", "abs_rms", "golden_rms", "tol_rel", "ok")}
         parity["golden"] = "tests/golden/pc_ouve.npz"
+        if r["dtype"] == "fp32":  # the north star's bound: 1e-4 absolute RMS on the complex spectrogram
+            parity["tol_abs"] = 1e-4
+            parity["ok"] = bool(parity["ok"] and r["abs_rms"] < 1e-4)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
@@ -516,8 +526,10 @@ def run(args):
     n_frames = 1 + int(args.seconds * SR) // 128
     T_frames = (n_frames + 63) // 64 * 64
     tag = args.config.upper()
-    if args.config == "c2" and (args.seconds != 4.0 or args.dtype != "bf16" or args.N != 30):
+    if args.config == "c2" and (args.seconds != 4.0 or args.N != 30):
         tag = "custom"
+    elif args.config == "c2" and args.dtype == "fp32":
+        tag = "C2-fp32"  # the C2 workload in the exact fp32 parity mode (the north star's 1e-4 tolerance)
     if rank == 0:
         if args.config == "c4":
             wl = (f"C4: B={B} {args.seconds:g} s/16 kHz clips per GPU, one-step SNR-aligned enhancement "

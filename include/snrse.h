@@ -47,6 +47,12 @@ void snrse_ctx_destroy(snrse_ctx* ctx);
 int snrse_ctx_set_workspace(snrse_ctx* ctx, void* ptr, size_t bytes);
 int snrse_ctx_set_option(snrse_ctx* ctx, const char* name, int value);
 int snrse_ctx_get_option(const snrse_ctx* ctx, const char* name, int* value);
+/* Diagnostic timing (bench.py's roofline probe): from now on every snrse_conv2d call through ctx is
+ * bracketed by a pair of HIP events (created here, without the system-scope fence), up to `capacity`
+ * calls; capacity 0 stops and frees them.  snrse_ctx_probe_read waits for the recorded calls and writes,
+ * in call order, each call's device time in ms and the kernel generation that ran ("last_kernel"). */
+int snrse_ctx_probe_begin(snrse_ctx* ctx, int capacity);
+int snrse_ctx_probe_read(snrse_ctx* ctx, float* ms, int* kernel, int max, int* n);
 
 /* Generic FIR resampling on [major, in_h, in_w, minor] — replaces the reference's only
  * native op binding, upfirdn2d(input, kernel, up_x, up_y, down_x, down_y, pad_x0, pad_x1,
@@ -113,10 +119,11 @@ int snrse_gn_apply(const void* src0, int C0, const void* src1, int C1, int B, in
 int snrse_gn_resample(snrse_ctx* ctx, const void* src, int C, int B, int H, int W, const float* scale, const float* shift,
                       int act, int mode, void* out_act, void* out_raw, hipStream_t stream);
 
-/* Elementwise GroupNorm-apply (+SiLU) of the channel concatenation (src0 | src1), bf16, from
- * precomputed scale/shift [B][C0+C1] (both NULL: identity).  out [B][HW][C0+C1]. */
+/* Elementwise GroupNorm-apply (+SiLU) of the channel concatenation (src0 | src1), dtype SNRSE_BF16 or
+ * SNRSE_F32 (exact SiLU), from precomputed scale/shift [B][C0+C1] (snrse_gn_scale_shift; both NULL:
+ * identity).  out [B][HW][C0+C1]. */
 int snrse_gn_act(const void* src0, int C0, const void* src1, int C1, int B, int HW, const float* scale,
-                 const float* shift, int act, void* out, hipStream_t stream);
+                 const float* shift, int act, void* out, int dtype, hipStream_t stream);
 
 /* Split-K workspace of the small-image conv GEMMs (levels whose tile grid underfills the CUs) of the
  * process default context (per context: snrse_ctx_set_workspace): a device buffer of `bytes` the

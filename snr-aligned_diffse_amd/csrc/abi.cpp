@@ -81,6 +81,75 @@ int set_workspace(snrse_ctx& c, void* ptr, size_t bytes) {
 
 __attribute__((visibility("hidden"))) snrse_ctx* snrse_ctx_resolve(snrse_ctx* c) { return c ? c : &g_default_ctx; }
 
+namespace {
+void probe_free(snrse_ctx& c) {
+  for (int i = 0; i < 2 * c.probe_cap; ++i) (void)hipEventDestroy(c.probe_ev[i]);
+  delete[] c.probe_ev;
+  delete[] c.probe_kernel;
+  c.probe_ev = nullptr;
+  c.probe_kernel = nullptr;
+  c.probe_cap = c.probe_n = 0;
+}
+}  // namespace
+
+__attribute__((visibility("hidden"))) int snrse_ctx_probe_mark(snrse_ctx& c, hipStream_t s, bool end) {
+  if (c.probe_n >= c.probe_cap) return 0;
+  if (end) {
+    c.probe_kernel[c.probe_n] = c.last_kernel;
+    return (int)hipEventRecord(c.probe_ev[2 * c.probe_n++ + 1], s);
+  }
+  return (int)hipEventRecord(c.probe_ev[2 * c.probe_n], s);
+}
+
+// Diagnostic timing of snrse_conv2d calls: `capacity` event pairs, created without the system-scope
+// fence (an event whose record flushes the caches to system scope puts that write-back inside the
+// bracket: ~50 us per fp32 conv call at C5, profiles/r03g_c5_probe_vs_rocprof.json).  capacity 0 frees them.
+extern "C" int snrse_ctx_probe_begin(snrse_ctx* ctx, int capacity) {
+  snrse_ctx& c = *snrse_ctx_resolve(ctx);
+  probe_free(c);
+  if (capacity <= 0) return 0;
+  c.probe_ev = new (std::nothrow) hipEvent_t[2 * (size_t)capacity];
+  c.probe_kernel = new (std::nothrow) int[capacity];
+  if (!c.probe_ev || !c.probe_kernel) {
+    delete[] c.probe_ev;
+    delete[] c.probe_kernel;
+    c.probe_ev = nullptr;
+    c.probe_kernel = nullptr;
+    return (int)hipErrorOutOfMemory;
+  }
+  for (int i = 0; i < 2 * capacity; ++i) {
+    const hipError_t e = hipEventCreateWithFlags(&c.probe_ev[i], hipEventDisableSystemFence);
+    if (e != hipSuccess) {
+      c.probe_cap = i / 2;
+      for (int j = 2 * c.probe_cap; j < i; ++j) (void)hipEventDestroy(c.probe_ev[j]);
+      probe_free(c);
+      return (int)e;
+    }
+  }
+  c.probe_cap = capacity;
+  c.probe_n = 0;
+  return 0;
+}
+
+// Waits for the probed calls and writes, in call order, each call's device time (ms, first kernel start
+// to last kernel end of the call) and the kernel generation that ran; *n = number of calls recorded.
+extern "C" int snrse_ctx_probe_read(snrse_ctx* ctx, float* ms, int* kernel, int max, int* n) {
+  snrse_ctx& c = *snrse_ctx_resolve(ctx);
+  if (!n) return SNRSE_EINVAL;
+  const int m = c.probe_n < max ? c.probe_n : max;
+  for (int i = 0; i < m; ++i) {
+    hipError_t e = hipEventSynchronize(c.probe_ev[2 * i + 1]);
+    if (e != hipSuccess) return (int)e;
+    if (ms) {
+      e = hipEventElapsedTime(&ms[i], c.probe_ev[2 * i], c.probe_ev[2 * i + 1]);
+      if (e != hipSuccess) return (int)e;
+    }
+    if (kernel) kernel[i] = c.probe_kernel[i];
+  }
+  *n = m;
+  return 0;
+}
+
 // A new context starts with the process default context's switches (so SNRSE_OPTS / snrse_set_option
 // settings made before carry over), no workspace and cleared read-backs.
 extern "C" snrse_ctx* snrse_ctx_create(void) {
@@ -92,10 +161,16 @@ extern "C" snrse_ctx* snrse_ctx_create(void) {
   c->last_ksplit = 1;
   c->last_epi_nt = 0;
   c->last_chunks = 1;
+  c->probe_ev = nullptr;
+  c->probe_kernel = nullptr;
+  c->probe_cap = c->probe_n = 0;
   return c;
 }
 
-extern "C" void snrse_ctx_destroy(snrse_ctx* ctx) { delete ctx; }
+extern "C" void snrse_ctx_destroy(snrse_ctx* ctx) {
+  if (ctx) probe_free(*ctx);
+  delete ctx;
+}
 
 extern "C" int snrse_ctx_set_workspace(snrse_ctx* ctx, void* ptr, size_t bytes) {
   return set_workspace(*snrse_ctx_resolve(ctx), ptr, bytes);

@@ -95,7 +95,13 @@ struct snrse_ctx {
   size_t ws_bytes = 0;
   // read-backs of the latest launch through this context
   int last_kernel = 0, last_ksplit = 1, last_epi_nt = 0, last_chunks = 1;
+  // diagnostic timing (snrse_ctx_probe_begin): an event pair around each snrse_conv2d call
+  hipEvent_t* probe_ev = nullptr;  // [2 * probe_cap]
+  int* probe_kernel = nullptr;     // [probe_cap] generation that ran
+  int probe_cap = 0, probe_n = 0;
 };
+// bracket one snrse_conv2d call with the context's next probe event pair (no-op when probing is off)
+int snrse_ctx_probe_mark(snrse_ctx& c, hipStream_t s, bool end);
 // `c`, or the process default context when c == NULL
 snrse_ctx* snrse_ctx_resolve(snrse_ctx* c);
 SNRSE_DEV size_t stat_idx(int b, int slot, int c, int C) {

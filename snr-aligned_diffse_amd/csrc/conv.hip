@@ -1292,6 +1292,12 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
   const long long per_img = (long long)H * W * std::max(std::max(C0, C1), std::max(p.Csc, p.Csc1)) * esz;
   constexpr long long kLim = 0x7ff00000ll;
   cx.last_chunks = 1;
+  SNRSE_RET((hipError_t)snrse_ctx_probe_mark(cx, stream, false));
+  struct ProbeEnd {  // closes the probe bracket on every return path below
+    snrse_ctx& c;
+    hipStream_t s;
+    ~ProbeEnd() { (void)snrse_ctx_probe_mark(c, s, true); }
+  } probe_end{cx, stream};
   if (per_img * B < kLim || per_img >= kLim) return run(p);
   const int chunk = (int)((kLim - 1) / per_img);
   cx.last_chunks = (B + chunk - 1) / chunk;

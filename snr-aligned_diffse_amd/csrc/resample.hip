@@ -197,11 +197,15 @@ __global__ __launch_bounds__(256) void gn_resample_kernel(const bf16_t* __restri
 
 // out [B][HW][C0 + C1] = act(x * scale + shift) of the channel concatenation (src0 | src1).
 // grid (nblk, B): each block stages its image's scale / shift in LDS.
-__global__ __launch_bounds__(256) void gn_act_kernel(const bf16_t* __restrict__ src0, int C0,
-                                                     const bf16_t* __restrict__ src1, int C1, int HW,
+// T = bf16 (fast SiLU: v_exp + v_rcp, far below the bf16 rounding of the result) or float (the fp32
+// parity mode: x / (1 + exp(-x)) as torch computes it); one 16-B vector per thread (8 bf16 / 4 f32)
+template <typename T>
+__global__ __launch_bounds__(256) void gn_act_kernel(const T* __restrict__ src0, int C0,
+                                                     const T* __restrict__ src1, int C1, int HW,
                                                      int pix_per_blk, const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int act,
-                                                     bf16_t* __restrict__ out) {
+                                                     T* __restrict__ out) {
+  constexpr int V = 16 / (int)sizeof(T);
   extern __shared__ __attribute__((aligned(16))) float s_ss[];  // scale[C], shift[C]
   const int C = C0 + C1;
   const int b = blockIdx.y;
@@ -210,22 +214,33 @@ __global__ __launch_bounds__(256) void gn_act_kernel(const bf16_t* __restrict__ 
     s_ss[C + c] = scale ? shift[(size_t)b * C + c] : 0.f;
   }
   __syncthreads();
-  const int LP = C / 8;
+  const int LP = C / V;
   const int p0 = blockIdx.x * pix_per_blk;
   const int p1 = min(HW, p0 + pix_per_blk);
   const int total = (p1 - p0) * LP;
   for (int idx = threadIdx.x; idx < total; idx += 256) {
     const int pix = p0 + idx / LP;
-    const int c = (idx % LP) * 8;
-    const bf16_t* s = c < C0 ? src0 + ((size_t)b * HW + pix) * C0 + c : src1 + ((size_t)b * HW + pix) * C1 + (c - C0);
-    float x[8];
-    unpack8(*(const u32x4*)s, x);
+    const int c = (idx % LP) * V;
+    const T* s = c < C0 ? src0 + ((size_t)b * HW + pix) * C0 + c : src1 + ((size_t)b * HW + pix) * C1 + (c - C0);
+    const u32x4 raw = *(const u32x4*)s;
+    u32x4 o;
+    if constexpr (sizeof(T) == 2) {
+      float x[8];
+      unpack8(raw, x);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float y = fmaf(x[i], s_ss[c + i], s_ss[C + c + i]);
-      x[i] = act ? silu(y) : y;
+      for (int i = 0; i < 8; ++i) {
+        const float y = fmaf(x[i], s_ss[c + i], s_ss[C + c + i]);
+        x[i] = act ? silu(y) : y;
+      }
+      o = pack8(x);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float y = fmaf(__uint_as_float(raw[i]), s_ss[c + i], s_ss[C + c + i]);
+        o[i] = __float_as_uint(act ? silu_exact(y) : y);
+      }
     }
-    *(u32x4*)(out + ((size_t)b * HW + pix) * C + c) = pack8(x);
+    *(u32x4*)(out + ((size_t)b * HW + pix) * C + c) = o;
   }
 }
 
@@ -557,16 +572,22 @@ extern "C" int snrse_gn_resample(snrse_ctx* ctx, const void* src, int C, int B, 
 }
 
 extern "C" int snrse_gn_act(const void* src0, int C0, const void* src1, int C1, int B, int HW, const float* scale,
-                            const float* shift, int act, void* out, hipStream_t stream) {
+                            const float* shift, int act, void* out, int dtype, hipStream_t stream) {
   const int C = C0 + C1;
-  if (!src0 || !out || C0 <= 0 || C0 % 8 || C1 < 0 || C1 % 8 || (C1 > 0 && !src1) || B <= 0 || HW <= 0 ||
+  if (dtype != SNRSE_BF16 && dtype != SNRSE_F32) return SNRSE_EINVAL;
+  const int V = dtype == SNRSE_BF16 ? 8 : 4;
+  if (!src0 || !out || C0 <= 0 || C0 % V || C1 < 0 || C1 % V || (C1 > 0 && !src1) || B <= 0 || HW <= 0 ||
       (!scale) != (!shift) || C > 4096)
     return SNRSE_EINVAL;
-  const int LP = C / 8;
+  const int LP = C / V;
   int ppb = (8 * 256) / LP;  // ~8 vectors per thread
   if (ppb < 1) ppb = 1;
   dim3 grid((HW + ppb - 1) / ppb, B);
-  hipLaunchKernelGGL(gn_act_kernel, grid, dim3(256), sizeof(float) * 2 * C, stream, (const bf16_t*)src0, C0,
-                     (const bf16_t*)src1, C1, HW, ppb, scale, shift, act, (bf16_t*)out);
+  if (dtype == SNRSE_BF16)
+    hipLaunchKernelGGL(gn_act_kernel<bf16_t>, grid, dim3(256), sizeof(float) * 2 * C, stream, (const bf16_t*)src0, C0,
+                       (const bf16_t*)src1, C1, HW, ppb, scale, shift, act, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(gn_act_kernel<float>, grid, dim3(256), sizeof(float) * 2 * C, stream, (const float*)src0, C0,
+                       (const float*)src1, C1, HW, ppb, scale, shift, act, (float*)out);
   return (int)hipGetLastError();
 }

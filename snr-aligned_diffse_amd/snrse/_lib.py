@@ -45,12 +45,14 @@ SIGNATURES = {
     "snrse_snrnet": [_vp, _i, _i] + [_vp] * 17 + [_vp, _vp, _vp],
     "snrse_istft": [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
     "snrse_gn_resample": [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp],
-    "snrse_gn_act": [_vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp],
+    "snrse_gn_act": [_vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp],
     "snrse_set_workspace": [_vp, C.c_size_t],
     # caller-owned launch contexts (snrse_ctx: switches, split-K workspace, read-backs)
     "snrse_ctx_set_workspace": [_vp, _vp, C.c_size_t],
     "snrse_ctx_set_option": [_vp, C.c_char_p, _i],
     "snrse_ctx_get_option": [_vp, C.c_char_p, _vp],
+    "snrse_ctx_probe_begin": [_vp, _i],
+    "snrse_ctx_probe_read": [_vp, _vp, _vp, _i, _vp],
     # consistency-training step (csrc/train.hip)
     "snrse_conv_wgrad": [_vp, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp],
     "snrse_chan_sum": [_vp, _i, _i, _i, _vp, _vp, _f, _vp],

@@ -166,6 +166,22 @@ def get_option(name):
     return context().get_option(name)
 
 
+def probe_begin(capacity, dev=None):
+    """Bracket the next `capacity` conv2d calls of this thread's current context with library-recorded HIP
+    events (snrse_ctx_probe_begin; created without the system-scope fence).  capacity 0 stops probing."""
+    _lib.call("snrse_ctx_probe_begin", context(dev).ptr, int(capacity))
+
+
+def probe_read(max_calls, dev=None):
+    """(ms per probed conv2d call, kernel generation per call), in call order (snrse_ctx_probe_read)."""
+    ms = (C.c_float * max_calls)()
+    kern = (C.c_int * max_calls)()
+    n = C.c_int(0)
+    _lib.call("snrse_ctx_probe_read", context(dev).ptr, C.addressof(ms), C.addressof(kern), int(max_calls),
+              C.addressof(n))
+    return list(ms[:n.value]), list(kern[:n.value])
+
+
 KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 5: "conv_halo5_kernel", 10: "conv_head_kernel"}
 
 
@@ -316,8 +332,9 @@ def gn_apply(src0, src1=None, sums=None, gamma=None, beta=None, act=True, mode="
     C1 = 0 if src1 is None else src1.shape[3]
     C = C0 + C1
     m = MODES[mode]
-    if src0.dtype == torch.bfloat16 and sums is not None:
-        # bf16: the per-(b, c) affine once, then the elementwise / LDS-tiled apply
+    if sums is not None and (m == 0 or src0.dtype == torch.bfloat16):
+        # the per-(b, c) affine once (snrse_gn_scale_shift), then the elementwise / LDS-tiled apply: no
+        # per-block re-fold of the slotted statistics (the fp32 gn_apply pass ran at ~0.2 of HBM peak that way)
         scale, shift = gn_scale_shift(sums, gamma, beta, H * W, sums1=sums1, groups=groups, eps=eps)
         if m == 0:
             return gn_act(src0, src1, scale, shift, act=act)
@@ -351,15 +368,13 @@ def gn_resample(x, scale=None, shift=None, act=True, mode="down", want_raw=False
 
 
 def gn_act(src0, src1=None, scale=None, shift=None, act=True):
-    """act(x*scale+shift) of the channel concatenation (src0 | src1), NHWC bf16 (snrse_gn_act)."""
+    """act(x*scale+shift) of the channel concatenation (src0 | src1), NHWC bf16 or f32 (snrse_gn_act)."""
     _dev(src0, src1, scale, shift)
-    if src0.dtype != torch.bfloat16:
-        raise TypeError("snrse: gn_act takes bf16 activations")
     B, H, W, C0 = src0.shape
     C1 = 0 if src1 is None else src1.shape[3]
     out = torch.empty(B, H, W, C0 + C1, device=src0.device, dtype=src0.dtype)
     _lib.call("snrse_gn_act", src0.data_ptr(), C0, _ptr(src1), C1, B, H * W, _ptr(scale), _ptr(shift),
-              int(bool(act)), out.data_ptr(), _stream())
+              int(bool(act)), out.data_ptr(), code(src0.dtype), _stream())
     return out
 
 
