@@ -199,11 +199,6 @@ SNRSE_DEV float sum_lanes_strided(float v) {
 // bias / temb / Combine weights are per-lane constants and no row or column masking is needed.
 // Epilogue flags as a compile-time mask (EF >= 0: the v5 halo GEMM's common configurations, no
 // per-pass branches) or read from the parameters at run time (EF = -1).
-enum { EF_TEMB = 1, EF_RES = 2, EF_COMB = 4, EF_STATS = 8, EF_NT = 16, EF_RT = -1 };
-inline int epi_flags(const ConvParams& p) {  // host side (launch dispatch)
-  return (p.temb ? EF_TEMB : 0) | (p.res ? EF_RES : 0) | (p.comb_src ? EF_COMB : 0) | (p.stats ? EF_STATS : 0) |
-         (p.epi_nt ? EF_NT : 0);
-}
 
 template <typename TO, int NWM, int BN, bool DEFER, int EF = EF_RT>
 SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int mb, int nb, int lane, float* stage,
@@ -838,7 +833,6 @@ __global__ __launch_bounds__(256) void conv_splitk_finalize(ConvParams p, int pp
 // halo 396 rows x 64 B (25 KB, register-staged with the fused GroupNorm+SiLU) + a 2-slot ring of
 // 3-tap weight phases (2 x 24 KB, LDS-DMA) = 72.75 KB, so two workgroups share a CU and one's
 // prologue / epilogue runs under the other's MFMAs (v4 is 1 workgroup/CU, 152 KB).
-SNRSE_DEV int swz64(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >> 1) & 3)) << 4); }
 
 #ifndef SNRSE_H5_OPAQUE
 #define SNRSE_H5_OPAQUE 0

@@ -94,6 +94,18 @@ SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
 int launch_head(const ConvParams& p, hipStream_t s);
 bool head_ok(const ConvParams& p);
 
+// Epilogue flags as a compile-time mask (EF >= 0: the halo GEMMs' common configurations, no per-pass
+// branches) or read from the parameters at run time (EF = -1).
+enum { EF_TEMB = 1, EF_RES = 2, EF_COMB = 4, EF_STATS = 8, EF_NT = 16, EF_RT = -1 };
+inline int epi_flags(const ConvParams& p) {  // host side (launch dispatch)
+  return (p.temb ? EF_TEMB : 0) | (p.res ? EF_RES : 0) | (p.comb_src ? EF_COMB : 0) | (p.stats ? EF_STATS : 0) |
+         (p.epi_nt ? EF_NT : 0);
+}
+
+// Halo image rows of 64 B (32 bf16 channels), 16-B chunk swizzled by (row >> 1) & 3: conflict-free
+// ds_read_b128 lane groups for any 16 consecutive rows.
+SNRSE_DEV int swz64(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >> 1) & 3)) << 4); }
+
 // GroupNorm prologue of the halo kernels (v5 GEMM, pyramid head) on one 16-B vector (8 bf16 channels): GNM 1 = affine,
 // 2 = affine + SiLU; `ok` = inside the image (else the conv's zero padding).  Written stage by stage
 // over the 8 elements (8 independent exp / rcp chains) so the schedule can hide the transcendental
