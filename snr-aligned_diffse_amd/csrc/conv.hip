@@ -934,7 +934,11 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 #undef SNRSE_HALO5_LOADS
   auto gn_publish = [&]() {  // before the barrier that precedes halo_store
     if constexpr (GNM > 0) {
-      if (tid < 16) *(f32x4*)(gnl + tid * 4) = gnv;
+      if (tid < 16) {
+        f32x4 g = gnv;
+        if constexpr (GNM == 2) g *= kNegLog2e;  // gn_xform8's prescaled SiLU affine
+        *(f32x4*)(gnl + tid * 4) = g;
+      }
     }
   };
   auto halo_store = [&](int c) {

@@ -110,47 +110,17 @@ SNRSE_DEV int swz64(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >>
 // 2 = affine + SiLU; `ok` = inside the image (else the conv's zero padding).  Written stage by stage
 // over the 8 elements (8 independent exp / rcp chains) so the schedule can hide the transcendental
 // latencies; element by element the chain was fully serial with an s_nop after every exp and rcp.
-#ifndef SNRSE_XF_PACKED
-#define SNRSE_XF_PACKED 0
-#endif
-typedef __attribute__((ext_vector_type(2))) float f32x2;
+//
+// GNM 2 takes the affine PRESCALED by -log2(e) (gn_silu_prescale): with z = -y log2(e),
+//   SiLU(y) = y / (1 + 2^-y log2 e) = z * rcp(-(1 + 2^z) / ln 2),
+// so the exp argument needs no multiply and 1 + 2^z folds its scale into one fma: 5 VALU per element
+// (fma, exp, fma, rcp, mul) instead of 6.  z -> +inf gives -0 (SiLU's limit), z -> -inf gives y.
+constexpr float kNegLog2e = -1.44269504088896341f;
+constexpr float kNegInvLn2 = -1.44269504088896341f;  // -1 / ln 2 (= -log2 e)
+SNRSE_DEV float gn_silu_prescale(float v) { return v * kNegLog2e; }
 
 template <int GNM>
 SNRSE_DEV u32x4 gn_xform8(const u32x4 v, const float* sc, const float* sh, bool ok) {
-#if SNRSE_XF_PACKED
-  // packed-f32 form: the affine, the exp argument, 1 + e and the product run as v_pk_fma / v_pk_mul /
-  // v_pk_add on element pairs (one wave-instruction per 2 elements)
-  f32x2 y[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f32x2 xv = {__uint_as_float(v[i] << 16), __uint_as_float(v[i] & 0xffff0000u)};
-    const f32x2 s = {sc[2 * i], sc[2 * i + 1]}, t = {sh[2 * i], sh[2 * i + 1]};
-    y[i] = __builtin_elementwise_fma(xv, s, t);
-  }
-  if constexpr (GNM == 2) {
-    f32x2 e[4];
-    const f32x2 nl2e = {-1.44269504088896341f, -1.44269504088896341f}, one = {1.0f, 1.0f};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const f32x2 z = y[i] * nl2e;
-      e[i] = f32x2{__builtin_amdgcn_exp2f(z[0]), __builtin_amdgcn_exp2f(z[1])};
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const f32x2 d = e[i] + one;
-      e[i] = f32x2{__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) y[i] = y[i] * e[i];
-  }
-  const uint32_t okm = 0u - (uint32_t)ok;
-  u32x4 o;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = pack_bf16x2(y[i][0], y[i][1]) & okm;
-  return o;
-#else
   float y[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -158,14 +128,14 @@ SNRSE_DEV u32x4 gn_xform8(const u32x4 v, const float* sc, const float* sh, bool 
     y[2 * i + 1] = fmaf(__uint_as_float(v[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]);
   }
   if constexpr (GNM == 2) {
-    // sched_barrier(0) between the stages: without it the scheduler (at the kernel's 256-VGPR limit)
-    // re-serialises the 8 chains to save registers
+    // y holds z here.  sched_barrier(0) between the stages: without it the scheduler (at the
+    // kernel's 256-VGPR limit) re-serialises the 8 chains to save registers
     float e[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_exp2f(y[k] * -1.44269504088896341f);
+    for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_exp2f(y[k]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_rcpf(1.0f + e[k]);
+    for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_rcpf(fmaf(e[k], kNegInvLn2, kNegInvLn2));
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < 8; ++k) y[k] *= e[k];
@@ -176,7 +146,6 @@ SNRSE_DEV u32x4 gn_xform8(const u32x4 v, const float* sc, const float* sh, bool 
 #pragma unroll
   for (int i = 0; i < 4; ++i) o[i] = pack_bf16x2(y[2 * i], y[2 * i + 1]) & okm;
   return o;
-#endif
 }
 
 }  // namespace snrse_conv

@@ -44,6 +44,9 @@ SNRSE_DEV int kh_swz(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >
       gs1 = *(const f32x4*)(sp_ + 4);                                                                          \
       gh0 = *(const f32x4*)hp_;                                                                                \
       gh1 = *(const f32x4*)(hp_ + 4);                                                                          \
+      if (GNM == 2) { /* gn_xform8's prescaled SiLU affine */                                                  \
+        gs0 *= kNegLog2e; gs1 *= kNegLog2e; gh0 *= kNegLog2e; gh1 *= kNegLog2e;                               \
+      }                                                                                                        \
     }                                                                                                          \
   } while (0)
 
