@@ -138,6 +138,7 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  * "splitk" 0 disables the split-K small-image GEMMs, "splitk_target" workgroups a split launch aims for;
  * "epi_nt" 0 / 1 / 2 (auto above "epi_nt_mb" = 256 MB of output) non-temporal halo-GEMM output stores;
  * "h5_specialise" 1 compile-time epilogue flags for the NCSN++ ResBlock configurations;
+ * "h5_tw" halo-GEMM tile: 0 auto (8 rows x 32 px where H % 8 == 0, else 4 x 64), 64 forces 4 x 64;
  * "resample_variant" 0 row-strip / 1 LDS-tiled gn_resample, "resample_nt" non-temporal stores there,
  * "resample_down_rows" 1 / 2 (default) / 4 output rows per down-sampling row strip (bit-identical results);
  * "stats_zeroed" 1 = the statistics buffers handed to snrse_conv2d / snrse_gn_stats are already zero (the
@@ -147,7 +148,8 @@ int snrse_set_option(const char* name, int value);
 /* Read back a switch (any name above) or: "halo_kernel" = generation of the halo conv kernel the current
  * setting dispatches to (5), "last_kernel" = generation of the most recent snrse_conv2d launch (1 v1, 2 v2,
  * 5 halo, 10 pyramid head), "last_ksplit" = K splits of the most recent v2 launch, "last_epi_nt" /
- * "last_chunks" = store flavour / image-range launches of the most recent halo conv. */
+ * "last_chunks" = store flavour / image-range launches of the most recent halo conv, "last_tw" = its tile
+ * width (32 / 64). */
 int snrse_get_option(const char* name, int* value);
 
 /* AttnBlockpp attention core (layerspp.py:84-88): qkv [B][L][3C] -> out [B][L][C],

@@ -43,6 +43,7 @@ int* option_field(snrse_ctx& c, const char* name) {
   if (name_is(name, "epi_nt")) return &c.epi_nt;
   if (name_is(name, "epi_nt_mb")) return &c.epi_nt_mb;
   if (name_is(name, "h5_specialise")) return &c.h5_specialise;
+  if (name_is(name, "h5_tw")) return &c.h5_tw;
   if (name_is(name, "stats_zeroed")) return &c.stats_zeroed;
   if (name_is(name, "resample_variant")) return &c.resample_variant;
   if (name_is(name, "resample_nt")) return &c.resample_nt;
@@ -68,6 +69,7 @@ int get_option(const snrse_ctx& c, const char* name, int* value) {
   if (name_is(name, "last_ksplit")) { *value = c.last_ksplit; return 0; }
   if (name_is(name, "last_epi_nt")) { *value = c.last_epi_nt; return 0; }
   if (name_is(name, "last_chunks")) { *value = c.last_chunks; return 0; }
+  if (name_is(name, "last_tw")) { *value = c.last_tw; return 0; }
   return SNRSE_EINVAL;
 }
 
@@ -161,6 +163,7 @@ extern "C" snrse_ctx* snrse_ctx_create(void) {
   c->last_ksplit = 1;
   c->last_epi_nt = 0;
   c->last_chunks = 1;
+  c->last_tw = 0;
   c->probe_ev = nullptr;
   c->probe_kernel = nullptr;
   c->probe_cap = c->probe_n = 0;

@@ -86,6 +86,7 @@ struct snrse_ctx {
   int epi_nt = 2;              // halo-GEMM non-temporal output stores: 0 off, 1 on, 2 above epi_nt_mb
   int epi_nt_mb = 256;         // MB of output above which epi_nt = 2 streams (the Infinity Cache size)
   int h5_specialise = 1;       // compile-time epilogue flags for the common bf16 configurations
+  int h5_tw = 0;               // halo tile width: 0 auto (32 where H % 8 == 0), 64, 32
   int stats_zeroed = 0;        // statistics buffers arrive zeroed (the caller clears one arena)
   int resample_variant = 0;    // 0 row-strip, 1 LDS-tiled gn_resample
   int resample_nt = 0;         // non-temporal stores in gn_resample
@@ -94,7 +95,7 @@ struct snrse_ctx {
   float* ws = nullptr;
   size_t ws_bytes = 0;
   // read-backs of the latest launch through this context
-  int last_kernel = 0, last_ksplit = 1, last_epi_nt = 0, last_chunks = 1;
+  int last_kernel = 0, last_ksplit = 1, last_epi_nt = 0, last_chunks = 1, last_tw = 0;
   // diagnostic timing (snrse_ctx_probe_begin): an event pair around each snrse_conv2d call
   hipEvent_t* probe_ev = nullptr;  // [2 * probe_cap]
   int* probe_kernel = nullptr;     // [probe_cap] generation that ran

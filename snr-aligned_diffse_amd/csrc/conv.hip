@@ -194,15 +194,21 @@ SNRSE_DEV float sum_lanes_strided(float v) {
   return __uint_as_float(r2[0]) + __uint_as_float(r2[1]);
 }
 
-// Lean LDS-staged epilogue of the halo kernels: the wave's 64 rows are 64 consecutive pixels of
-// image `b` and its 64 channels are in range (H % 4 == 0, W % 64 == 0, Cout % 128 == 0 there), so
-// bias / temb / Combine weights are per-lane constants and no row or column masking is needed.
+// Lean LDS-staged epilogue of the halo kernels: the wave's 64 rows are 64 / TW segments of TW
+// consecutive pixels in consecutive image rows of image `b` (pixel of wave row r: mb + r + (r / TW) *
+// seg_skip, seg_skip = W - TW), and its 64 channels are in range (H % 4 == 0, W % TW == 0, Cout % 128 == 0
+// there), so bias / temb / Combine weights are per-lane constants and no row or column masking is needed.
 // Epilogue flags as a compile-time mask (EF >= 0: the v5 halo GEMM's common configurations, no
 // per-pass branches) or read from the parameters at run time (EF = -1).
 
-template <typename TO, int NWM, int BN, bool DEFER, int EF = EF_RT>
+template <int TW>
+SNRSE_DEV int epi_pix(int mb, int row, int seg_skip) {
+  return TW == 64 ? mb + row : mb + row + (row / TW) * seg_skip;
+}
+
+template <typename TO, int NWM, int BN, bool DEFER, int EF = EF_RT, int TW = 64>
 SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int mb, int nb, int lane, float* stage,
-                            float* red, int wm, int b, int blk_n0) {
+                            float* red, int wm, int b, int blk_n0, int seg_skip = 0) {
   const bool f_temb = EF < 0 ? p.temb != nullptr : (EF & EF_TEMB) != 0;
   const bool f_res = EF < 0 ? p.res != nullptr : (EF & EF_RES) != 0;
   const bool f_comb = EF < 0 ? p.comb_src != nullptr : (EF & EF_COMB) != 0;
@@ -261,11 +267,12 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
     if (f_res) {
 #pragma unroll
       for (int pass = 0; pass < NPASS; ++pass)
-        rpre[pass] = *(const u32x4*)((const TO*)p.res + ((size_t)mb + r0 + pass * RPP) * p.res_ld + n);
+        rpre[pass] = *(const u32x4*)((const TO*)p.res + (size_t)epi_pix<TW>(mb, r0 + pass * RPP, seg_skip) * p.res_ld + n);
     }
     if (f_comb) {
 #pragma unroll
-      for (int pass = 0; pass < NPASS; ++pass) qpre[pass] = *(const f32x4*)(p.comb_src + ((size_t)mb + r0 + pass * RPP) * 4);
+      for (int pass = 0; pass < NPASS; ++pass)
+        qpre[pass] = *(const f32x4*)(p.comb_src + (size_t)epi_pix<TW>(mb, r0 + pass * RPP, seg_skip) * 4);
     }
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -273,7 +280,7 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
 #pragma unroll
   for (int pass = 0; pass < NPASS; ++pass) {
     const int row = r0 + pass * RPP;
-    const size_t m = (size_t)mb + row;
+    const size_t m = (size_t)epi_pix<TW>(mb, row, seg_skip);
     float v[EPC];
     const float* sr = stage + row * LDR + cc * EPC;
 #pragma unroll
@@ -293,8 +300,10 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
         for (int k = 0; k < 4; ++k) v[k] += __uint_as_float(rv[k]);
       }
     }
+    if (p.out_scale != 1.f) {  // (uniform: Conv_0 and the other unscaled convs skip the multiply)
 #pragma unroll
-    for (int k = 0; k < EPC; ++k) v[k] *= p.out_scale;
+      for (int k = 0; k < EPC; ++k) v[k] *= p.out_scale;
+    }
     if (f_comb) {
       f32x4 q;
       if constexpr (PRE) q = qpre[pass];
@@ -828,11 +837,13 @@ __global__ __launch_bounds__(256) void conv_splitk_finalize(ConvParams p, int pp
 }
 
 // ---------------------------------------------------------------------------------------------
-// v5 halo GEMM, two workgroups per CU.  4 waves; tile = 4 image rows x 64 px x 128 couts; wave w
-// computes output row h0+w (64 px) x all 128 couts (acc 128 VGPRs).  K runs in 32-channel chunks:
-// halo 396 rows x 64 B (25 KB, register-staged with the fused GroupNorm+SiLU) + a 2-slot ring of
-// 3-tap weight phases (2 x 24 KB, LDS-DMA) = 72.75 KB, so two workgroups share a CU and one's
-// prologue / epilogue runs under the other's MFMAs (v4 is 1 workgroup/CU, 152 KB).
+// v5 halo GEMM, two workgroups per CU.  4 waves; tile = TH image rows x TW px x 128 couts (TH x TW =
+// 256: 4 x 64 or 8 x 32); wave w computes 64 px (output rows h0 + w TH/4 ..) x all 128 couts (acc 128
+// VGPRs).  K runs in 32-channel chunks: halo (TH+2)(TW+2) rows x 64 B (4 x 64: 396 rows, 25 KB; 8 x 32:
+// 340 rows, 21 KB), register-staged with the fused GroupNorm+SiLU, + a 2-slot ring of 3-tap weight
+// phases (2 x 24 KB, LDS-DMA), so two workgroups share a CU and one's prologue / epilogue runs under
+// the other's MFMAs (v4 is 1 workgroup/CU, 152 KB).  The 8 x 32 tile has 14 % fewer halo rows per
+// output pixel (340 vs 396): 14 % less GroupNorm+SiLU transform VALU and halo traffic.
 
 #ifndef SNRSE_H5_OPAQUE
 #define SNRSE_H5_OPAQUE 0
@@ -843,11 +854,12 @@ SNRSE_DEV int h5_opaque(int v) {
   return r;
 }
 
-template <typename TO, int GNM, int EF>
+template <typename TO, int GNM, int EF, int TW>
 __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
-  constexpr int TH = 4, TW = 64, HC = TW + 2;
-  constexpr int HROWS = (TH + 2) * HC;  // 396
-  constexpr int HJ = 7;                 // halo rows per thread: (tid >> 2) + 64 j
+  constexpr int TH = 256 / TW, HC = TW + 2;
+  constexpr int RW = TH / 4;                // image rows per wave
+  constexpr int HROWS = (TH + 2) * HC;      // 396 (4 x 64) / 340 (8 x 32)
+  constexpr int HJ = (HROWS + 63) / 64;     // halo rows per thread: (tid >> 2) + 64 j
   constexpr int HALO_BYTES = HROWS * 64;
   constexpr int TAPB = 128 * 64;  // one tap's 128 couts x 32 ch bf16
   constexpr int SLOT = 3 * TAPB;
@@ -1024,11 +1036,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
     for (int jt = 0; jt < nt; ++jt) {
       const int tp = t0 + jt;
       const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
-      const int hbase = (wid + dy + 1) * HC + dx + 1 + lrow;
+      const int hbase = (wid * RW + dy + 1) * HC + dx + 1 + lrow;
       const char* sb = sl + jt * TAPB;
       u32x4 af[4], bfr[8];
+      // fragment i: pixels 16 i .. 16 i + 15 of the wave's 64 = image row (16 i) / TW, column (16 i) % TW
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = *(const u32x4*)(halo + swz64(hbase + i * 16, lg));
+      for (int i = 0; i < 4; ++i) af[i] = *(const u32x4*)(halo + swz64(hbase + (16 * i / TW) * HC + (16 * i) % TW, lg));
 #pragma unroll
       for (int j = 0; j < 8; ++j) bfr[j] = *(const u32x4*)(sb + swz64(j * 16 + lrow, lg));
 #pragma unroll
@@ -1052,12 +1065,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   __builtin_amdgcn_s_barrier();  // LDS is reused as the epilogue staging area
   float* const stage = (float*)(smem + wid * (64 * 68 * 4));
   float* const red = (float*)(smem + 4 * (64 * 68 * 4));
-  const int mrow = (bb * p.H + h0 + wid) * p.W + w0;
-  epilogue_img<TO, 4, 128, true, EF>(p, acc[0], mrow, n0, lane, stage, red, wid, bb, n0);
+  const int mrow = (bb * p.H + h0 + wid * RW) * p.W + w0;
+  epilogue_img<TO, 4, 128, true, EF, TW>(p, acc[0], mrow, n0, lane, stage, red, wid, bb, n0, p.W - TW);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
   SNRSE_STAMP(26);
-  epilogue_img<TO, 4, 128, true, EF>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0);
+  epilogue_img<TO, 4, 128, true, EF, TW>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0, p.W - TW);
   SNRSE_STAMP(27);
   if (EF < 0 ? p.stats != nullptr : (EF & EF_STATS) != 0) block_stats_flush<4, 128>(p, red, bb, n0);
 #ifdef SNRSE_STAMPS
@@ -1081,26 +1094,29 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 #endif
 }
 
-template <typename TO, int GNM, int EF>
-int launch_halo5_ef(ConvParams p, int grid, size_t lds, hipStream_t s) {
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_halo5_kernel<TO, GNM, EF>,
+template <typename TO, int GNM, int EF, int TW>
+int launch_halo5_ef(ConvParams p, int grid, hipStream_t s) {
+  // halo + weight ring + (stamps build: 4 x 32 stamps) + the next chunk's GroupNorm affine (2 x 32 f32),
+  // and at least the epilogue's reuse of it: 4 waves' 64 x 68 f32 staging + the 4 x 128 x 2 f32 statistics
+  constexpr size_t main_lds = (256 / TW + 2) * (TW + 2) * 64 + 2 * 3 * 128 * 64 + 1024 + 256;
+  constexpr size_t epi_lds = 4 * (64 * 68 * 4) + 4 * 128 * 2 * 4;
+  constexpr size_t lds = main_lds > epi_lds ? main_lds : epi_lds;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_halo5_kernel<TO, GNM, EF, TW>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   SNRSE_RET(attr);  // (thread-safe one-time set: a function-local static)
-  hipLaunchKernelGGL((conv_halo5_kernel<TO, GNM, EF>), dim3(grid), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((conv_halo5_kernel<TO, GNM, EF, TW>), dim3(grid), dim3(256), lds, s, p);
   return (int)hipGetLastError();
 }
 
-template <typename TO, int GNM>
+template <typename TO, int GNM, int TW>
 int launch_halo5_gn(ConvParams p, hipStream_t s, snrse_ctx& cx) {
-  // halo + weight ring + (stamps build: 4 x 32 stamps) + the next chunk's GroupNorm affine (2 x 32 f32)
-  constexpr size_t lds = 396 * 64 + 2 * 3 * 128 * 64 + 1024 + 256;
   p.ntn = p.Cout / 128;
   // non-temporal output stores when the output exceeds the 256 MB Infinity Cache (+1 % on the
   // full-resolution convs)
   p.epi_nt = cx.epi_nt == 2 ? ((long long)p.M * p.out_ld * (long long)sizeof(TO) > ((long long)cx.epi_nt_mb << 20))
                             : cx.epi_nt;
   cx.last_epi_nt = p.epi_nt;
-  const int tiles = p.B * (p.H / 4) * (p.W / 64) * p.ntn;
+  const int tiles = p.B * (p.H / (256 / TW)) * (p.W / TW) * p.ntn;
   const int grid = tiles;
   // the bf16 ResBlock configurations of the NCSN++ path get a branch-free epilogue (bias always on):
   // Conv_0 (+temb), Conv_1 (+residual | +1x1 shortcut as extra K | +Combine), each +-stats, +-NT
@@ -1108,7 +1124,7 @@ int launch_halo5_gn(ConvParams p, hipStream_t s, snrse_ctx& cx) {
     if (cx.h5_specialise && p.bias) {
       switch (epi_flags(p)) {
 #define SNRSE_H5_EF(F) \
-  case (F): return launch_halo5_ef<TO, GNM, (F)>(p, grid, lds, s);
+  case (F): return launch_halo5_ef<TO, GNM, (F), TW>(p, grid, s);
         SNRSE_H5_EF(EF_TEMB | EF_STATS)
         SNRSE_H5_EF(EF_TEMB | EF_STATS | EF_NT)
         SNRSE_H5_EF(EF_RES | EF_STATS)
@@ -1122,15 +1138,23 @@ int launch_halo5_gn(ConvParams p, hipStream_t s, snrse_ctx& cx) {
       }
     }
   }
-  return launch_halo5_ef<TO, GNM, EF_RT>(p, grid, lds, s);
+  return launch_halo5_ef<TO, GNM, EF_RT, TW>(p, grid, s);
 }
 
-// GroupNorm prologue mode as a template argument: the halo transform is straight-line code
+// GroupNorm prologue mode and tile width as template arguments: the halo transform is straight-line
+// code.  Tile 8 x 32 where H % 8 == 0 (option h5_tw: 0 auto, 64 / 32 force where legal), else 4 x 64.
+template <typename TO, int TW>
+int launch_halo5_tw(ConvParams p, hipStream_t s, snrse_ctx& cx) {
+  cx.last_tw = TW;
+  if (!p.gn_scale) return launch_halo5_gn<TO, 0, TW>(p, s, cx);
+  if (!p.gn_act) return launch_halo5_gn<TO, 1, TW>(p, s, cx);
+  return launch_halo5_gn<TO, 2, TW>(p, s, cx);
+}
+
 template <typename TO>
 int launch_halo5(ConvParams p, hipStream_t s, snrse_ctx& cx) {
-  if (!p.gn_scale) return launch_halo5_gn<TO, 0>(p, s, cx);
-  if (!p.gn_act) return launch_halo5_gn<TO, 1>(p, s, cx);
-  return launch_halo5_gn<TO, 2>(p, s, cx);
+  if (cx.h5_tw != 64 && p.H % 8 == 0) return launch_halo5_tw<TO, 32>(p, s, cx);
+  return launch_halo5_tw<TO, 64>(p, s, cx);
 }
 
 // K splits for a v2 launch of `tiles` output tiles over nk K-tiles: about one workgroup per CU when

@@ -404,11 +404,12 @@ def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     (8, 256, 0, 256, 64, 128, 0, 0, True, True, False, True),      # two Cout tiles per image
     (2, 256, 256, 256, 32, 64, 0, 0, False, False, True, False),   # cat input, no GN
 ])
-@pytest.mark.parametrize("variant", [5])
-def test_conv_halo_large(gpu, case, variant):
-    """The halo GEMMs (v5, v7) vs an fp32 torch reference on the GPU at multi-image sizes, with
-    the fused GroupNorm+SiLU prologue, cat inputs, the 1x1 shortcut, temb, residual and the
-    per-channel output statistics."""
+@pytest.mark.parametrize("tw", [0, 64])
+def test_conv_halo_large(gpu, case, tw):
+    """The halo GEMM (v5, both tiles: 8 x 32 auto where H % 8 == 0, 4 x 64 forced) vs an fp32 torch
+    reference on the GPU at multi-image sizes, with the fused GroupNorm+SiLU prologue, cat inputs, the
+    1x1 shortcut, temb, residual and the per-channel output statistics."""
+    variant = 5
     from snrse import ops
     B, C0, C1, Co, H, W, Csc, Csc1, use_gn, use_temb, use_res, use_st = case
     g = torch.Generator(device=gpu).manual_seed(sum(case[:8]))
@@ -443,13 +444,17 @@ def test_conv_halo_large(gpu, case, variant):
     ref = ref * scale
     st = ops.new_stats(B, Co) if use_st else None
     ops.set_option("conv_variant", variant)
+    ops.set_option("h5_tw", tw)
     try:
         out = ops.conv2d(x0, w.reshape(Co, -1).contiguous(), 3, Co, bias=bias, src1=x1, sc=xs0, sc1=xs1, sc_wgt=ws,
                          temb=temb, temb_off=40, res=res, out_scale=scale, stats=st, gn=gn)
         ran = ops.kernel_name(ops.get_option("last_kernel"))
+        ran_tw = ops.get_option("last_tw")
     finally:
         ops.set_option("conv_variant", 0)
+        ops.set_option("h5_tw", 0)
     assert ran == f"conv_halo{variant}_kernel"
+    assert ran_tw == (tw or (32 if H % 8 == 0 else 64))
     got = out.float().permute(0, 3, 1, 2)
     assert rel(got, ref) < 1e-2
     if use_st:
