@@ -140,7 +140,7 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  * "h5_specialise" 1 compile-time epilogue flags for the NCSN++ ResBlock configurations;
  * "h5_tw" halo-GEMM tile: 0 auto (8 rows x 32 px where H % 8 == 0, else 4 x 64), 64 forces 4 x 64;
  * "resample_variant" 0 row-strip / 1 LDS-tiled gn_resample, "resample_nt" non-temporal stores there,
- * "resample_down_rows" 1 / 2 (default) / 4 output rows per down-sampling row strip (bit-identical results);
+ * "resample_down_rows" 1 / 2 / 4 (default) output rows per down-sampling row strip (bit-identical results);
  * "stats_zeroed" 1 = the statistics buffers handed to snrse_conv2d / snrse_gn_stats are already zero (the
  * caller clears one arena per network evaluation), so they skip their per-call memset. */
 int snrse_set_option(const char* name, int value);

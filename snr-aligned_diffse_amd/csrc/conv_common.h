@@ -115,9 +115,7 @@ SNRSE_DEV int swz64(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >>
 //   SiLU(y) = y / (1 + 2^-y log2 e) = z * rcp(-(1 + 2^z) / ln 2),
 // so the exp argument needs no multiply and 1 + 2^z folds its scale into one fma: 5 VALU per element
 // (fma, exp, fma, rcp, mul) instead of 6.  z -> +inf gives -0 (SiLU's limit), z -> -inf gives y.
-constexpr float kNegLog2e = -1.44269504088896341f;
-constexpr float kNegInvLn2 = -1.44269504088896341f;  // -1 / ln 2 (= -log2 e)
-SNRSE_DEV float gn_silu_prescale(float v) { return v * kNegLog2e; }
+SNRSE_DEV float gn_silu_prescale(float v) { return v * kNegLog2e; }  // (kNegLog2e: common.h)
 
 template <int GNM>
 SNRSE_DEV u32x4 gn_xform8(const u32x4 v, const float* sc, const float* sh, bool ok) {

@@ -5,16 +5,19 @@
 // channels; here the (4+2) x (64+2) halo of each 32-channel chunk is staged once (GroupNorm+SiLU
 // applied in registers, zero padding kept), all 9 taps read it from LDS, and the next chunk's halo
 // is loaded into registers under the current chunk's MFMAs.  The kernel is bound by one HBM pass
-// over h; each wave owns one image row of 64 px x 16 channels (4 of them real).
+// over h and the GroupNorm+SiLU VALU; tile 8 rows x 32 px (halo 10 x 34 = 340 rows: 14 % fewer
+// transformed halo vectors per pixel than 4 x 64's 396), each wave owns 2 image rows x 32 px x 16
+// channels (4 of them real).
 #include "conv_common.h"
 
 namespace snrse_conv {
 namespace {
 
-constexpr int KH_TH = 4, KH_TW = 64, KH_HC = KH_TW + 2;
-constexpr int KH_HROWS = (KH_TH + 2) * KH_HC;  // 396
-constexpr int KH_HJ = 7;                       // halo rows per thread: (tid >> 2) + 64 j
-constexpr int KH_HALO = KH_HROWS * 64;         // 25344 B
+constexpr int KH_TH = 8, KH_TW = 32, KH_HC = KH_TW + 2;
+constexpr int KH_RW = KH_TH / 4;                // image rows per wave
+constexpr int KH_HROWS = (KH_TH + 2) * KH_HC;  // 340
+constexpr int KH_HJ = (KH_HROWS + 63) / 64;    // halo rows per thread: (tid >> 2) + 64 j
+constexpr int KH_HALO = KH_HROWS * 64;         // 21760 B
 constexpr int KH_WP = 9 * 16 * 4;              // 16-B weight pieces of one chunk: 9 taps x 16 co x 4
 constexpr int KH_WJ = (KH_WP + 255) / 256;     // per thread (3)
 constexpr int KH_LDS = KH_HALO + 9 * 1024;     // + 9 taps x 16 co x 64 B = 34560 B
@@ -114,11 +117,11 @@ __global__ __launch_bounds__(256) void conv_head_kernel(ConvParams p) {
 #pragma unroll
     for (int tp = 0; tp < 9; ++tp) {
       const int dy = tp / 3 - 1, dx = tp % 3 - 1;
-      const int hbase = (wid + dy + 1) * KH_HC + dx + 1 + lrow;
+      const int hbase = (wid * KH_RW + dy + 1) * KH_HC + dx + 1 + lrow;
       const u32x4 a = *(const u32x4*)(wsl + tp * 1024 + kh_swz(lrow, lg));
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const u32x4 bx = *(const u32x4*)(halo + kh_swz(hbase + 16 * i, lg));
+      for (int i = 0; i < 4; ++i) {  // pixels 16 i .. of the wave's 64: row (16 i) / TW, column (16 i) % TW
+        const u32x4 bx = *(const u32x4*)(halo + kh_swz(hbase + (16 * i / KH_TW) * KH_HC + (16 * i) % KH_TW, lg));
         acc[i] = mfma_chunk<bf16_t>(a, bx, acc[i]);
       }
     }
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(256) void conv_head_kernel(ConvParams p) {
     if (p.bias) add = f32x4{p.bias[co], p.bias[co + 1], p.bias[co + 2], p.bias[co + 3]};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const size_t m = ((size_t)b * p.H + h0 + wid) * p.W + w0 + 16 * i + lrow;
+      const size_t m = ((size_t)b * p.H + h0 + wid * KH_RW + 16 * i / KH_TW) * p.W + w0 + (16 * i) % KH_TW + lrow;
       f32x4 v = acc[i] + add;
       if (p.res) v += *(const f32x4*)((const float*)p.res + m * p.res_ld + co);
       v *= p.out_scale;

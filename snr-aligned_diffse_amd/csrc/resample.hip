@@ -320,11 +320,13 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
   static_assert(MODE == MODE_DOWN || RD == 1, "multi-row strips: down only");
   const int orow = (ls / nseg) * RD;  // (first) output row
   const int Ho = MODE == MODE_DOWN ? H / 2 : 2 * H, Wo = MODE == MODE_DOWN ? W / 2 : 2 * W;
+  // with act: the affine prescaled by -log2(e) for silu_z (common.h)
+  const float pre = act ? kNegLog2e : 1.f;
   float sc[CPT], sh[CPT];
 #pragma unroll
   for (int i = 0; i < CPT; ++i) {
-    sc[i] = scale ? scale[(size_t)b * C + CPT * v + i] : 1.f;
-    sh[i] = scale ? shift[(size_t)b * C + CPT * v + i] : 0.f;
+    sc[i] = (scale ? scale[(size_t)b * C + CPT * v + i] : 1.f) * pre;
+    sh[i] = (scale ? shift[(size_t)b * C + CPT * v + i] : 0.f) * pre;
   }
   const __amdgpu_buffer_rsrc_t rsrc = rs_rsrc(src + (size_t)b * H * W * C, (unsigned)((size_t)H * W * C * 2));
   constexpr int NR = MODE == MODE_DOWN ? 2 * RD + 2 : 2;  // input rows of the strip's RD output rows
@@ -360,7 +362,9 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
     return rw;
   };
   // down: column values of the RD output rows (row rr takes input rows 2 rr .. 2 rr + 3 of the strip
-  // with the vertical taps [1,3,3,1]/8); each input vector is transformed once
+  // with the vertical taps [1,3,3,1]/8); each input vector is transformed once.  Zero padding: rows
+  // outside the image are skipped (their raw loads are 0 too) and an outside column's activated values
+  // are cleared once per column, not per element.
   auto eval_cols = [&](const Raw& rw, int ix, RowVec<CPT> (&cv)[RD]) {
     const bool colok = ix >= 0 && ix < W;
     constexpr float kv[4] = {0.125f, 0.375f, 0.375f, 0.125f};
@@ -370,13 +374,13 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
       for (int i = 0; i < CPT; ++i) { cv[rr].a[i] = 0.f; cv[rr].r[i] = 0.f; }
 #pragma unroll
     for (int a = 0; a < NR; ++a) {
+      if (!rowok[a]) continue;
       float x[CPT];
       V::unpack(rw.x[a], x);
-      const bool ok = colok && rowok[a];
 #pragma unroll
       for (int i = 0; i < CPT; ++i) {
-        const float y = fmaf(x[i], sc[i], sh[i]);
-        const float t = ok ? (act ? silu(y) : y) : 0.f;
+        const float z = fmaf(x[i], sc[i], sh[i]);
+        const float t = act ? silu_z(z) : z;
 #pragma unroll
         for (int rr = 0; rr < RD; ++rr) {
           const int k = a - 2 * rr;
@@ -387,6 +391,12 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
         }
       }
     }
+    if (!colok) {
+#pragma unroll
+      for (int rr = 0; rr < RD; ++rr)
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) cv[rr].a[i] = 0.f;
+    }
   };
   auto eval_col = [&](const Raw& rw, int ix) {
     const bool colok = ix >= 0 && ix < W;
@@ -395,16 +405,20 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
     for (int i = 0; i < CPT; ++i) { cv.a[i] = 0.f; cv.r[i] = 0.f; }
 #pragma unroll
     for (int a = 0; a < NR; ++a) {
+      if (!rowok[a]) continue;
       float x[CPT];
       V::unpack(rw.x[a], x);
-      const bool ok = colok && rowok[a];
 #pragma unroll
       for (int i = 0; i < CPT; ++i) {
-        const float y = fmaf(x[i], sc[i], sh[i]);
-        const float t = ok ? (act ? silu(y) : y) : 0.f;
+        const float z = fmaf(x[i], sc[i], sh[i]);
+        const float t = act ? silu_z(z) : z;
         cv.a[i] = fmaf(t, wy[a], cv.a[i]);
         cv.r[i] = fmaf(x[i], wy[a], cv.r[i]);
       }
+    }
+    if (!colok) {
+#pragma unroll
+      for (int i = 0; i < CPT; ++i) cv.a[i] = 0.f;
     }
     return cv;
   };
@@ -433,8 +447,9 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
       for (int rr = 0; rr < RD; ++rr)
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
-          pa[rr][i] = 0.125f * c0[rr].a[i] + 0.375f * c1[rr].a[i];
-          pr[rr][i] = 0.125f * c0[rr].r[i] + 0.375f * c1[rr].r[i];
+          // explicit fmaf: the same rounding sequence in every RD instantiation (no contraction choice)
+          pa[rr][i] = fmaf(0.375f, c1[rr].a[i], 0.125f * c0[rr].a[i]);
+          pr[rr][i] = fmaf(0.375f, c1[rr].r[i], 0.125f * c0[rr].r[i]);
         }
     }
     Raw n2 = load_col(2 * ox0 + 1), n3 = load_col(2 * ox0 + 2);

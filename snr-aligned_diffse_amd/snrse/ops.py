@@ -207,7 +207,7 @@ def head_ok(x):
     """True when a bf16 3x3 conv of x with Cout <= 16 and f32 output (the pyramid heads) takes the
     halo-staged head kernel, which accepts a fused GroupNorm (gn=)."""
     B, H, W, C = x.shape
-    return x.dtype == torch.bfloat16 and H % 4 == 0 and W % 64 == 0 and C % 32 == 0 and _VARIANT["v"] != 1
+    return x.dtype == torch.bfloat16 and H % 8 == 0 and W % 32 == 0 and C % 32 == 0 and _VARIANT["v"] != 1
 
 
 def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):

@@ -2,7 +2,7 @@
 """Micro-benchmark of the HBM-bound kernels of one NCSN++ evaluation at the C2 shapes (B=32, 4 s):
 gn_resample down / up at every level, the fused input conv, gn_act.  HIP events on the launch stream,
 median of --reps; achieved = algorithmic bytes (each tensor read or written once) / time.
-Usage: python tools/hbm_bench.py [--reps 20] [--only down,up,input,act]"""
+Usage: python tools/hbm_bench.py [--reps 20] [--only down,up,input,act,head,copy] [--levels 0,1]"""
 import argparse
 import json
 import os
@@ -40,7 +40,8 @@ def main():
     ap.add_argument("--only", default="down,up,input,act")
     ap.add_argument("--resample-variant", type=int, default=0)
     ap.add_argument("--nt", type=int, default=0)
-    ap.add_argument("--down-rows", type=int, default=2, help="option resample_down_rows (1, 2, 4)")
+    ap.add_argument("--down-rows", type=int, default=4, help="option resample_down_rows (1, 2, 4)")
+    ap.add_argument("--levels", default="", help="comma list of pyramid levels for down / up / head (default all)")
     a = ap.parse_args()
     ops.set_option("resample_down_rows", a.down_rows)
     ops.set_option("resample_variant", a.resample_variant)
@@ -54,6 +55,8 @@ def main():
         if kind not in only:
             continue
         lv = range(0, 6) if kind == "down" else range(1, 7)
+        if a.levels:
+            lv = [int(v) for v in a.levels.split(",") if int(v) in lv]
         for li in lv:
             H, W, C = LEVELS[li]
             x = torch.randn(B, H, W, C, device=dev, generator=g).bfloat16()
@@ -89,6 +92,22 @@ def main():
         byt = B * F * T * (16 + 256 + 16)  # x, y read; h bf16 + pyramid f32 written
         rows.append({"kernel": "input_conv", "shape": [B, F, T], "us": ms * 1e3, "bytes": byt,
                      "TBps": byt / ms / 1e9})
+    if "head" in only:  # level pyramid head: SiLU(GN(h)) -> conv3x3 C -> 4 (f32) + upsampled pyramid
+        for li in ([int(v) for v in a.levels.split(",")] if a.levels else range(0, 4)):
+            H, W, C = LEVELS[li]
+            x = torch.randn(B, H, W, C, device=dev, generator=g).bfloat16()
+            sc = torch.rand(B, C, device=dev, generator=g) + 0.5
+            sh = torch.randn(B, C, device=dev, generator=g)
+            w = (torch.randn(16, 9 * C, device=dev, generator=g) / 48).bfloat16()
+            w[4:] = 0
+            bias = torch.zeros(4, device=dev)
+            r = torch.randn(B, H, W, 4, device=dev, generator=g)
+            assert ops.head_ok(x)
+            ms = timed(lambda: ops.conv2d(x, w, 3, 4, bias=bias, res=r, out_f32=True, gn=(sc, sh)), a.reps)
+            byt = x.numel() * 2 + 2 * r.numel() * 4
+            rows.append({"kernel": "conv_head_gn", "shape": [B, H, W, C], "us": ms * 1e3, "bytes": byt,
+                         "TBps": byt / ms / 1e9})
+            del x, r
     if "act" in only:
         for li in (4, 5, 6):
             H, W, C = LEVELS[li]
