@@ -217,6 +217,41 @@ def oracle_one_step(y, sd, ssd, noise, fixed_snr=0.17783, sigma_max=0.5):
     return spec_ref.istft(spec_ref.spec_back(s[0, 0].numpy()), y.shape[1]) * norm, t_hat
 
 
+def cpu_baseline_train(frames=256, steps=1):
+    """--config train's CPU leg: the oracle's consistency-training step (oracle/train_ref.py: the loss of
+    model.py:361-390 on the NCSN++ restatement, torch autograd backward, pinned to the reference's own
+    autograd by tests/test_oracle_golden.py::test_train_step) + torch.optim.Adam over the trainable tensors,
+    for ONE [256, frames] spectrogram pair per step (the GPU leg's per-sample work), after one warm-up step."""
+    from oracle import ncsnpp_ref, train_ref
+    env = _cpu_env()
+    sd = ncsnpp_ref.state_dict_to_torch({k: v.numpy() for k, v in formula_weights().items()})
+    gen = torch.Generator().manual_seed(0)
+    noise = _complex_noise(gen)
+    x = noise((1, 1, 256, frames)) * 0.4
+    y = x + noise((1, 1, 256, frames)) * 0.4
+    params = [v for k, v in sd.items() if k not in train_ref.FROZEN]
+    for v in params:
+        v.requires_grad_(True)
+    opt = torch.optim.Adam(params, lr=1e-4)
+
+    def step(n):
+        opt.zero_grad(set_to_none=True)
+        loss = train_ref.consistency_loss(sd, x, y, noise(x.shape), torch.tensor([n]))
+        loss.backward()
+        opt.step()
+        return loss
+
+    step(5)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(3 + i)
+    el = (time.perf_counter() - t0) / steps
+    return {"value": 1.0 / el, "unit": "samples/s", "cores": env["cores"], "kind": "port",
+            "sample": (f"{steps} oracle consistency-training step(s) (CPU restatement, fp32) on ONE [256, {frames}] "
+                       f"spectrogram pair: 2 NCSN++ evaluations + autograd backward + torch Adam; {el:.2f} s/sample"),
+            "cpu_model": env["cpu_model"], "os_cpu_count": env["os_cpu_count"]}
+
+
 def cpu_baseline_c4(seconds=4.0, n=3):
     """C4's CPU leg: `n` synthetic clips through the oracle's one-step SNR-aligned enhance (SNRNet
     estimate + one fp32 NCSN++ evaluation + STFT / iSTFT), after one warm-up clip."""
@@ -418,6 +453,8 @@ def run_train(args):
                                     "evaluations + backward + fused Adam/EMA"), "global_batch": B, "per_gpu_batch": B,
                        "seq_len": T, "parallelism": "dp1"},
             "roofline": roof, "cpu_baseline": None, "loss": float(loss)}
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_train(frames=T)
     print(json.dumps(line), flush=True)
 
 

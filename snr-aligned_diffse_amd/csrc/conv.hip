@@ -1151,9 +1151,12 @@ int launch_halo5_tw(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   return launch_halo5_gn<TO, 2, TW>(p, s, cx);
 }
 
+inline bool halo_tile32(const ConvParams& p) { return p.H % 8 == 0 && p.W % 32 == 0; }
+inline bool halo_tile64(const ConvParams& p) { return p.H % 4 == 0 && p.W % 64 == 0; }
+
 template <typename TO>
 int launch_halo5(ConvParams p, hipStream_t s, snrse_ctx& cx) {
-  if (cx.h5_tw != 64 && p.H % 8 == 0) return launch_halo5_tw<TO, 32>(p, s, cx);
+  if (halo_tile32(p) && (cx.h5_tw != 64 || !halo_tile64(p))) return launch_halo5_tw<TO, 32>(p, s, cx);
   return launch_halo5_tw<TO, 64>(p, s, cx);
 }
 
@@ -1228,7 +1231,7 @@ int dispatch_conv(const ConvParams& p, hipStream_t s, snrse_ctx& cx) {
       const bool fits = p.bytes0 < 0x7ff00000ll && p.bytes1 < 0x7ff00000ll && p.sc_bytes0 < 0x7ff00000ll &&
                         p.sc_bytes1 < 0x7ff00000ll;
       if (cx.conv_variant != 1 && fits) {
-        if (cx.conv_variant != 2 && p.ksize == 3 && p.H % 4 == 0 && p.W % 64 == 0) {
+        if (cx.conv_variant != 2 && p.ksize == 3 && (halo_tile32(p) || halo_tile64(p))) {
           cx.last_kernel = kHaloAuto;
           return launch_halo5<TO>(p, s, cx);
         }

@@ -199,8 +199,8 @@ def halo_ok(x, ksize, cout):
     """True when snrse_conv2d takes the halo path (and so accepts a fused GroupNorm).  Any batch size
     qualifies: sources beyond 2 GiB run as consecutive launches over image ranges (snrse_conv2d)."""
     B, H, W, C = x.shape
-    return (x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and H % 4 == 0 and W % 64 == 0
-            and _VARIANT["v"] in (0, 5))
+    tiles = (H % 8 == 0 and W % 32 == 0) or (H % 4 == 0 and W % 64 == 0)  # 8 x 32 or 4 x 64 tiles
+    return x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and tiles and _VARIANT["v"] in (0, 5)
 
 
 def head_ok(x):

@@ -180,3 +180,33 @@ def test_snap_and_normfac():
     clean_rms, noise_rms = 0.09034279194278529, 0.01521404836098084  # active_rms.txt row 1
     t = snrnet_ref.snap_t(noise_rms / clean_rms, 0.17783)
     assert abs(t - float(g["t_hat"])) < 1e-12
+
+
+@pytest.mark.parametrize("branch,loss_type", [("true", "mse"), ("fixed", "sqrt_mse")])
+def test_train_step(branch, loss_type):
+    """oracle/train_ref.py (the consistency-training loss + autograd on the NCSN++ restatement) vs the
+    reference module's own autograd (tests/golden/train_step.npz): loss, per-tensor gradient sums of
+    squares and the recorded gradient heads.  The attention key biases (NIN_1.b) get an analytically zero
+    gradient (softmax is invariant to a per-query constant): compared by norm, as in test_gpu_train."""
+    from oracle import train_ref
+    g = golden("train_step.npz")
+    sd = ncsnpp_ref.state_dict_to_torch(formula_sd("ncsnpp"))
+    B, Fq, Tn = 2, 256, 64
+    x = torch.from_numpy(fnormal("golden.train.x", (B, 1, Fq, Tn), complex_=True)) * 0.4
+    y = torch.from_numpy(fnormal("golden.train.y", (B, 1, Fq, Tn), complex_=True)) * 0.4 + x
+    z = torch.from_numpy(fnormal("golden.train.z", (B, 1, Fq, Tn), complex_=True))
+    key = loss_type if branch == "true" else f"fixed_{loss_type}"
+    loss, grads = train_ref.loss_and_grads(sd, x, y, z, g["n"], branch, loss_type, float(g["fixed_snr"]))
+    assert abs(float(loss) / float(g[f"{key}_loss"]) - 1) < 3e-5
+    names = [str(k) for k in g["names"]]
+    head = int(g["head"])
+    got_sq = np.array([float((grads[k].double() ** 2).sum()) for k in names])
+    rel_sq = np.abs(got_sq - g[f"{key}_gsq"]) / np.maximum(g[f"{key}_gsq"], 1e-30)
+    for i, k in enumerate(names):
+        if k.endswith("NIN_1.b"):
+            sib = names.index(k.replace("NIN_1.b", "NIN_0.b"))
+            assert math.sqrt(got_sq[i] / g[f"{key}_gsq"][sib]) < 1e-5, k
+            rel_sq[i] = 0.0
+    assert rel_sq.max() < 2e-3, names[int(np.argmax(rel_sq))]
+    got_head = np.concatenate([grads[k].double().reshape(-1)[:head].numpy() for k in names])
+    assert rel(got_head, g[f"{key}_head"].astype(np.float64)) < 1e-3
