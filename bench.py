@@ -339,8 +339,9 @@ class ConvProbe:
 
     CAP = 4096
 
-    def __init__(self):
+    def __init__(self, all_threads=False):
         self.rec = []
+        self.all_threads = all_threads  # also the other threads' contexts (the autograd worker's backward)
 
     def install(self, ops):
         orig = ops.conv2d
@@ -353,15 +354,15 @@ class ConvProbe:
 
         ops.conv2d = wrapped
         self.orig, self.ops = orig, ops
-        ops.probe_begin(self.CAP)
+        ops.probe_begin(self.CAP, all_threads=self.all_threads)
 
     def uninstall(self):
         self.ops.conv2d = self.orig
 
     def summary(self):
         """{kernel: [flops, ms, launches]} over the probed pass."""
-        ms, kern = self.ops.probe_read(self.CAP)
-        self.ops.probe_begin(0)
+        ms, kern = self.ops.probe_read(self.CAP, all_threads=self.all_threads)
+        self.ops.probe_begin(0, all_threads=self.all_threads)
         if len(ms) != min(len(self.rec), self.CAP):
             raise RuntimeError(f"probe: {len(ms)} timed calls for {len(self.rec)} conv2d calls")
         if os.environ.get("SNRSE_PROBE_DUMP"):  # per-call record for tools/probe_reconcile.py
@@ -426,7 +427,7 @@ def run_train(args):
     for w in range(args.warmup):
         step(w)
     torch.cuda.synchronize()
-    probe = ConvProbe()
+    probe = ConvProbe(all_threads=True)  # the backward's dgrad convs run on the autograd worker thread
     t0 = time.perf_counter()
     for k in range(args.steps):
         loss = step(args.warmup + k)

@@ -1156,7 +1156,7 @@ inline bool halo_tile64(const ConvParams& p) { return p.H % 4 == 0 && p.W % 64 =
 
 template <typename TO>
 int launch_halo5(ConvParams p, hipStream_t s, snrse_ctx& cx) {
-  if (halo_tile32(p) && (cx.h5_tw != 64 || !halo_tile64(p))) return launch_halo5_tw<TO, 32>(p, s, cx);
+  if (halo_tile32(p) && cx.h5_tw != 64) return launch_halo5_tw<TO, 32>(p, s, cx);
   return launch_halo5_tw<TO, 64>(p, s, cx);
 }
 
@@ -1231,7 +1231,10 @@ int dispatch_conv(const ConvParams& p, hipStream_t s, snrse_ctx& cx) {
       const bool fits = p.bytes0 < 0x7ff00000ll && p.bytes1 < 0x7ff00000ll && p.sc_bytes0 < 0x7ff00000ll &&
                         p.sc_bytes1 < 0x7ff00000ll;
       if (cx.conv_variant != 1 && fits) {
-        if (cx.conv_variant != 2 && p.ksize == 3 && (halo_tile32(p) || halo_tile64(p))) {
+        // halo path on the 4 x 64-tileable images (levels 0-3 of the C2 pyramid), with 8 x 32 tiles where
+        // H % 8 == 0.  Not on W = 32 (level 4): 128 tiles for 512 workgroup slots ran 11-45 % slower there
+        // than the split-K LDS-DMA GEMM + gn_act (profiles/r03v_level4_halo_vs_glds.jsonl)
+        if (cx.conv_variant != 2 && p.ksize == 3 && halo_tile64(p)) {
           cx.last_kernel = kHaloAuto;
           return launch_halo5<TO>(p, s, cx);
         }

@@ -16,6 +16,7 @@ current context (so "last_kernel" etc. describe that thread's latest launch).
 from __future__ import annotations
 
 import ctypes as C
+import itertools
 import math
 import os
 import threading
@@ -51,6 +52,7 @@ def _ws_alloc(dev):
 
 
 _CONTEXTS = weakref.WeakSet()  # every live LaunchContext (set_option reaches all of them)
+_CTX_SEQ = itertools.count()
 _TLS = threading.local()       # per thread: {device: {lane: LaunchContext}}, current lane per device, arenas
 
 
@@ -70,6 +72,7 @@ class LaunchContext:
         _lib.call("snrse_ctx_set_workspace", self.ptr, None if self.ws is None else self.ws.data_ptr(),
                   0 if self.ws is None else mb << 20)
         self.zeroed = 0  # mirror of the context's "stats_zeroed" switch
+        self.seq = next(_CTX_SEQ)  # creation order (probe_read over several threads' contexts)
         _CONTEXTS.add(self)
 
     def set_option(self, name, value):
@@ -166,20 +169,37 @@ def get_option(name):
     return context().get_option(name)
 
 
-def probe_begin(capacity, dev=None):
-    """Bracket the next `capacity` conv2d calls of this thread's current context with library-recorded HIP
-    events (snrse_ctx_probe_begin; created without the system-scope fence).  capacity 0 stops probing."""
-    _lib.call("snrse_ctx_probe_begin", context(dev).ptr, int(capacity))
+def _probe_contexts(dev, all_threads):
+    """This thread's context first, then (all_threads) every other live context on the device by creation."""
+    own = context(dev)
+    if not all_threads:
+        return [own]
+    others = sorted((c for c in list(_CONTEXTS) if c is not own and c.device == own.device), key=lambda c: c.seq)
+    return [own] + others
 
 
-def probe_read(max_calls, dev=None):
-    """(ms per probed conv2d call, kernel generation per call), in call order (snrse_ctx_probe_read)."""
-    ms = (C.c_float * max_calls)()
-    kern = (C.c_int * max_calls)()
-    n = C.c_int(0)
-    _lib.call("snrse_ctx_probe_read", context(dev).ptr, C.addressof(ms), C.addressof(kern), int(max_calls),
-              C.addressof(n))
-    return list(ms[:n.value]), list(kern[:n.value])
+def probe_begin(capacity, dev=None, all_threads=False):
+    """Bracket the next `capacity` conv2d calls of this thread's current context (all_threads: of every
+    context on the device, e.g. the autograd engine's worker thread during a backward) with library-recorded
+    HIP events (snrse_ctx_probe_begin; created without the system-scope fence).  capacity 0 stops probing."""
+    for cx in _probe_contexts(dev, all_threads):
+        _lib.call("snrse_ctx_probe_begin", cx.ptr, int(capacity))
+
+
+def probe_read(max_calls, dev=None, all_threads=False):
+    """(ms per probed conv2d call, kernel generation per call) (snrse_ctx_probe_read): in call order for one
+    context; with all_threads, this thread's calls followed by each other context's (the order of a
+    training step: forward on the calling thread, then the backward on the autograd worker)."""
+    out_ms, out_k = [], []
+    for cx in _probe_contexts(dev, all_threads):
+        ms = (C.c_float * max_calls)()
+        kern = (C.c_int * max_calls)()
+        n = C.c_int(0)
+        _lib.call("snrse_ctx_probe_read", cx.ptr, C.addressof(ms), C.addressof(kern), int(max_calls),
+                  C.addressof(n))
+        out_ms += list(ms[:n.value])
+        out_k += list(kern[:n.value])
+    return out_ms, out_k
 
 
 KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 5: "conv_halo5_kernel", 10: "conv_head_kernel"}
@@ -199,8 +219,10 @@ def halo_ok(x, ksize, cout):
     """True when snrse_conv2d takes the halo path (and so accepts a fused GroupNorm).  Any batch size
     qualifies: sources beyond 2 GiB run as consecutive launches over image ranges (snrse_conv2d)."""
     B, H, W, C = x.shape
-    tiles = (H % 8 == 0 and W % 32 == 0) or (H % 4 == 0 and W % 64 == 0)  # 8 x 32 or 4 x 64 tiles
-    return x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and tiles and _VARIANT["v"] in (0, 5)
+    # images tileable by 4 x 64 (the kernel then uses 8 x 32 tiles where H % 8 == 0); W = 32 alone stays on
+    # the split-K GEMM (faster there: profiles/r03v_level4_halo_vs_glds.jsonl)
+    return (x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and H % 4 == 0 and W % 64 == 0
+            and _VARIANT["v"] in (0, 5))
 
 
 def head_ok(x):

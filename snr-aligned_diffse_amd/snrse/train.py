@@ -339,34 +339,61 @@ class _ScaleRows(torch.autograd.Function):
 
 
 # ----------------------------------------------------------------------------- attention
+ATTN_CHUNK_BYTES = 256 << 20  # transient score / probability matrices per batch chunk
+
+
+def _attn_chunks(B, L):
+    """Utterance ranges whose [chunk, L, L] f32 score matrix fits ATTN_CHUNK_BYTES (at least one)."""
+    cb = max(1, ATTN_CHUNK_BYTES // (L * L * 4))
+    return [(b0, min(B, b0 + cb)) for b0 in range(0, B, cb)]
+
+
+def _attn_probs(q, k, scale):
+    """P = softmax_rows(q k^T scale) of one batch chunk (the same kernels in forward and backward, so the
+    recomputed probabilities are bit-identical to the forward's)."""
+    B, L, Cc = q.shape
+    S = bgemm(q, (L * Cc, Cc, 1), k, (L * Cc, 1, Cc), L, L, Cc, batch=B)
+    P = torch.empty_like(S)
+    _call("snrse_softmax_rows", S.data_ptr(), P.data_ptr(), B * L, L, float(scale))
+    return P
+
+
 class _Attention(torch.autograd.Function):
     """o[l] = sum_m softmax_m(q[l] . k[m] C^-1/2) v[m] per utterance (AttnBlockpp, layerspp.py:84-88);
-    q, k, v [B, L, C]; the probabilities are kept for the backward (L <= a few thousand)."""
+    q, k, v [B, L, C].  Only q, k, v are kept for the backward, which recomputes the probabilities; both
+    passes walk the batch in chunks whose L x L matrices stay within ATTN_CHUNK_BYTES, so memory is bounded
+    for any sequence length (30 s clips: L = 16 x 236)."""
 
     @staticmethod
     def forward(ctx, q, k, v):
         q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
         B, L, Cc = q.shape
         scale = Cc ** -0.5
-        S = bgemm(q, (L * Cc, Cc, 1), k, (L * Cc, 1, Cc), L, L, Cc, batch=B)
-        P = torch.empty_like(S)
-        _call("snrse_softmax_rows", S.data_ptr(), P.data_ptr(), B * L, L, float(scale))
-        o = bgemm(P, (L * L, L, 1), v, (L * Cc, Cc, 1), L, Cc, L, batch=B)
-        ctx.save_for_backward(q, k, v, P)
+        o = torch.empty_like(q)
+        for b0, b1 in _attn_chunks(B, L):
+            P = _attn_probs(q[b0:b1], k[b0:b1], scale)
+            bgemm(P, (L * L, L, 1), v[b0:b1], (L * Cc, Cc, 1), L, Cc, L, batch=b1 - b0, C=o[b0:b1],
+                  sC=(L * Cc, Cc, 1))
+        ctx.save_for_backward(q, k, v)
         ctx.scale = scale
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, P = ctx.saved_tensors
+        q, k, v = ctx.saved_tensors
         do = do.contiguous()
         B, L, Cc = q.shape
-        dP = bgemm(do, (L * Cc, Cc, 1), v, (L * Cc, 1, Cc), L, L, Cc, batch=B)
-        dV = bgemm(P, (L * L, 1, L), do, (L * Cc, Cc, 1), L, Cc, L, batch=B)
-        dS = torch.empty_like(dP)
-        _call("snrse_softmax_bwd_rows", P.data_ptr(), dP.data_ptr(), dS.data_ptr(), B * L, L, float(ctx.scale))
-        dQ = bgemm(dS, (L * L, L, 1), k, (L * Cc, Cc, 1), L, Cc, L, batch=B)
-        dK = bgemm(dS, (L * L, 1, L), q, (L * Cc, Cc, 1), L, Cc, L, batch=B)
+        dQ, dK, dV = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        for b0, b1 in _attn_chunks(B, L):
+            n = b1 - b0
+            qc, kc, vc, doc = q[b0:b1], k[b0:b1], v[b0:b1], do[b0:b1]
+            P = _attn_probs(qc, kc, ctx.scale)
+            dP = bgemm(doc, (L * Cc, Cc, 1), vc, (L * Cc, 1, Cc), L, L, Cc, batch=n)
+            bgemm(P, (L * L, 1, L), doc, (L * Cc, Cc, 1), L, Cc, L, batch=n, C=dV[b0:b1], sC=(L * Cc, Cc, 1))
+            dS = torch.empty_like(dP)
+            _call("snrse_softmax_bwd_rows", P.data_ptr(), dP.data_ptr(), dS.data_ptr(), n * L, L, float(ctx.scale))
+            bgemm(dS, (L * L, L, 1), kc, (L * Cc, Cc, 1), L, Cc, L, batch=n, C=dQ[b0:b1], sC=(L * Cc, Cc, 1))
+            bgemm(dS, (L * L, 1, L), qc, (L * Cc, Cc, 1), L, Cc, L, batch=n, C=dK[b0:b1], sC=(L * Cc, Cc, 1))
         return dQ, dK, dV
 
 

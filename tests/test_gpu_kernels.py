@@ -403,8 +403,7 @@ def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     (4, 128, 0, 128, 256, 512, 128, 0, True, False, True, True),   # Conv_1 + shortcut
     (8, 256, 0, 256, 64, 128, 0, 0, True, True, False, True),      # two Cout tiles per image
     (2, 256, 256, 256, 32, 64, 0, 0, False, False, True, False),   # cat input, no GN
-    (8, 256, 0, 256, 16, 32, 0, 0, True, True, False, True),       # level 4 (W = 32: 8 x 32 tiles only)
-    (4, 256, 256, 256, 16, 32, 256, 256, True, False, False, True),  # level-4 up-path Conv_1 + cat shortcut
+    (4, 256, 256, 256, 16, 64, 256, 256, True, False, False, True),  # up-path Conv_1 + cat shortcut, 256 ch
 ])
 @pytest.mark.parametrize("tw", [0, 64])
 def test_conv_halo_large(gpu, case, tw):
@@ -456,8 +455,7 @@ def test_conv_halo_large(gpu, case, tw):
         ops.set_option("conv_variant", 0)
         ops.set_option("h5_tw", 0)
     assert ran == f"conv_halo{variant}_kernel"
-    t32, t64 = H % 8 == 0 and W % 32 == 0, H % 4 == 0 and W % 64 == 0
-    assert ran_tw == (32 if t32 and (tw != 64 or not t64) else 64)
+    assert ran_tw == (32 if H % 8 == 0 and tw != 64 else 64)
     got = out.float().permute(0, 3, 1, 2)
     assert rel(got, ref) < 1e-2
     if use_st:

@@ -200,3 +200,30 @@ def test_training_loop_runs_and_updates(gpu):
     assert not torch.equal(w0, m.dnn.all_modules[4].Conv_0.weight)
     assert torch.equal(gfp0, m.dnn.all_modules[0].W)
     assert m.ema.num_updates == 3 and len(m.ema.shadow_params) == 646
+
+
+@pytest.mark.parametrize("chunked", [False, True])
+def test_training_attention_vs_torch(gpu, chunked):
+    """snrse.train._Attention (HIP bgemm + softmax kernels, probabilities recomputed in the backward,
+    batch chunks bounded by ATTN_CHUNK_BYTES) vs torch autograd of softmax(q k^T / sqrt(C)) v in fp64."""
+    from snrse import train as tr
+    gen = torch.Generator(device=gpu).manual_seed(11)
+    B, L, C = 3, 192, 64
+    q, k, v = (torch.randn(B, L, C, device=gpu, generator=gen) for _ in range(3))
+    do = torch.randn(B, L, C, device=gpu, generator=gen)
+    old = tr.ATTN_CHUNK_BYTES
+    if chunked:
+        tr.ATTN_CHUNK_BYTES = L * L * 4  # one utterance per chunk
+    try:
+        qa, ka, va = (t.clone().requires_grad_(True) for t in (q, k, v))
+        o = tr._Attention.apply(qa, ka, va)
+        o.backward(do)
+    finally:
+        tr.ATTN_CHUNK_BYTES = old
+    assert len(tr._attn_chunks(B, L)) == 1 and (not chunked or L * L * 4 < old)
+    qr, kr, vr = (t.double().clone().requires_grad_(True) for t in (q, k, v))
+    orf = torch.softmax(qr @ kr.transpose(1, 2) / math.sqrt(C), -1) @ vr
+    orf.backward(do.double())
+    for got, ref in ((o, orf), (qa.grad, qr.grad), (ka.grad, kr.grad), (va.grad, vr.grad)):
+        err = (got.double() - ref).norm() / ref.norm()
+        assert err < 1e-5, float(err)
