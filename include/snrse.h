@@ -16,7 +16,9 @@
  *     argument); snrse_error_string() maps it to text.  The Python host maps non-zero to
  *     RuntimeError, as the reference's TORCH_CHECK does (op/upfirdn2d.cpp:8-19).
  *   - dtype: SNRSE_F32 = 0 (exact fp32 "parity" mode), SNRSE_BF16 = 1 (bf16 storage,
- *     fp32 accumulation).  Activations are NHWC: [B, F(=H), T(=W), C].
+ *     fp32 accumulation), SNRSE_F32X3 = 4 (snrse_conv2d only: fp32 activations and output, weights
+ *     pre-split into bf16 hi / lo halves, three bf16 MFMA products per K-tile -- the fast fp32
+ *     parity mode).  Activations are NHWC: [B, F(=H), T(=W), C].
  *   - Complex spectrograms are interleaved complex64 [B, F, T] (= the reference's
  *     [B, 1, F, T] tensors).
  */
@@ -32,7 +34,7 @@ extern "C" {
 
 typedef struct ihipStream_t* hipStream_t;
 
-enum { SNRSE_F32 = 0, SNRSE_BF16 = 1, SNRSE_F16 = 2, SNRSE_F64 = 3 };
+enum { SNRSE_F32 = 0, SNRSE_BF16 = 1, SNRSE_F16 = 2, SNRSE_F64 = 3, SNRSE_F32X3 = 4 };
 
 int snrse_abi_version(void); /* 2: snrse_ctx arguments */
 const char* snrse_error_string(int code);
@@ -82,7 +84,10 @@ int snrse_upfirdn2d(const void* in, void* out, const float* kernel, int major, i
  *          is consumed as SiLU(x*scale+shift) (gn_act=1) or x*scale+shift (gn_act=0), i.e. the
  *          ResBlock's GroupNorm+SiLU fused into the GEMM's halo load (bf16, 3x3, H%4==0,
  *          W%64==0, and the pyramid heads Cout<=16 with f32 output; otherwise
- *          hipErrorInvalidValue). */
+ *          hipErrorInvalidValue).
+ *   dtype SNRSE_F32X3: src/res/out fp32; wgt [Npad][2*ksize*ksize*(C0+C1)] and sc_wgt [Npad][2*(Csc+Csc1)]
+ *          bf16, each 32-element K-tile of the fp32 packing stored as 32 hi = bf16(w) then 32
+ *          lo = bf16(w - hi); Cout % 128 == 0, no gn_scale / out_f32 (else hipErrorInvalidValue). */
 int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void* src1, int C1, int B, int H, int W, int ksize,
                  const void* wgt, const void* sc_src, int Csc, const void* sc_src1, int Csc1,
                  const void* sc_wgt, const float* bias, const float* temb, int temb_stride,
@@ -141,6 +146,7 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  * "h5_tw" halo-GEMM tile: 0 auto (8 rows x 32 px where H % 8 == 0, else 4 x 64), 64 forces 4 x 64;
  * "resample_variant" 0 row-strip / 1 LDS-tiled gn_resample, "resample_nt" non-temporal stores there,
  * "resample_down_rows" 1 / 2 / 4 (default) output rows per down-sampling row strip (bit-identical results);
+ * "x3_tile" split-bf16 fp32 GEMM tile: 0 auto, 1 128 px x 128 couts, 2 256 x 128, 3 128 x 256 (Cout % 256 == 0);
  * "stats_zeroed" 1 = the statistics buffers handed to snrse_conv2d / snrse_gn_stats are already zero (the
  * caller clears one arena per network evaluation), so they skip their per-call memset. */
 int snrse_set_option(const char* name, int value);

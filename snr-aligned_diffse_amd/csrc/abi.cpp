@@ -48,6 +48,7 @@ int* option_field(snrse_ctx& c, const char* name) {
   if (name_is(name, "resample_variant")) return &c.resample_variant;
   if (name_is(name, "resample_nt")) return &c.resample_nt;
   if (name_is(name, "resample_down_rows")) return &c.resample_down_rows;
+  if (name_is(name, "x3_tile")) return &c.x3_tile;
   return nullptr;
 }
 

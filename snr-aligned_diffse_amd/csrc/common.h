@@ -74,7 +74,8 @@ SNRSE_DEV double wave_sum_d(double v) {
 }
 
 // dtype codes shared with the C-ABI (include/snrse.h)
-enum { SNRSE_F32 = 0, SNRSE_BF16 = 1, SNRSE_F16 = 2, SNRSE_F64 = 3 };  // F16 / F64: snrse_upfirdn2d only
+// F16 / F64: snrse_upfirdn2d only; F32X3: snrse_conv2d's split-bf16 fp32 GEMM (pre-split weights)
+enum { SNRSE_F32 = 0, SNRSE_BF16 = 1, SNRSE_F16 = 2, SNRSE_F64 = 3, SNRSE_F32X3 = 4 };
 
 // GroupNorm statistics buffers are [B][SNRSE_STAT_SLOTS][C][2] doubles: producers spread
 // their atomics over the slots (a few hundred workgroups per image would otherwise queue on
@@ -99,6 +100,7 @@ struct snrse_ctx {
   int resample_variant = 0;    // 0 row-strip, 1 LDS-tiled gn_resample
   int resample_nt = 0;         // non-temporal stores in gn_resample
   int resample_down_rows = 4;  // output rows per down-sampling row strip (1, 2, 4; 4 fastest since r03)
+  int x3_tile = 0;             // split-bf16 fp32 GEMM tile: 0 auto, 1 128x128, 2 256x128, 3 128x256
   // split-K workspace: [splits][M][Cout] f32 partial sums (NULL: no splitting)
   float* ws = nullptr;
   size_t ws_bytes = 0;

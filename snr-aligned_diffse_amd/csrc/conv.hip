@@ -566,6 +566,192 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma_kernel(ConvParams p) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Split-bf16 ("bf16x3") fp32 GEMM, the fast fp32 parity mode (dtype SNRSE_F32 with bf16 weights):
+// fp32 activations, weights pre-split on the host into hi = bf16(w), lo = bf16(w - hi), stored per
+// 32-element K-tile as one 128-B row [hi x 32 | lo x 32] ([Npad][2K] bf16).  The activation tile is
+// split the same way in registers on its way to LDS, and each K-tile accumulates
+//   A_hi B_hi + A_hi B_lo + A_lo B_hi
+// with three v_mfma_f32_16x16x32_bf16 (exact bf16 products, fp32 accumulation): the dropped lo*lo
+// term and the operands' residuals beyond 16 significant bits are ~2^-16 relative per product, and
+// one K-tile costs 48 MFMA cycles per 16x16 output block instead of the 256 of the eight
+// v_mfma_f32_16x16x4_f32 of the exact-fp32 kernel (measured: profiles/r03z_*).
+// Same tile walk, split-K and epilogues as the v1 kernel above; LDS rows use the same swizzle, with
+// the hi half in chunks 0-3 and the lo half in chunks 4-7.
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvParams p) {
+  constexpr int KT = 32;  // fp32 elements per K-tile
+  constexpr int NT = 64 * WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = TM / 16, FN = TN / 16;
+  constexpr int ROWS_PER_PASS = NT / 8;
+  constexpr int A_LD = (BM + ROWS_PER_PASS - 1) / ROWS_PER_PASS;
+  constexpr int B_LD = (BN + ROWS_PER_PASS - 1) / ROWS_PER_PASS;
+  static_assert(BM % 16 == 0 && BN % 16 == 0, "tile");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+#define AS(buf) (smem + (buf) * (BM * 128))
+#define BS(buf) (smem + 2 * BM * 128 + (buf) * (BN * 128))
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int nbk = gridDim.x, bid = blockIdx.x;
+  const int q8 = nbk >> 3, r8 = nbk & 7, xcd = bid & 7, pos = bid >> 3;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
+  const int ks = wg % p.ksplit, tl = wg / p.ksplit;
+  const int m0 = (tl / p.ntn) * BM;
+  const int n0 = (tl % p.ntn) * BN;
+  const int HW = p.H * p.W;
+  const int Cin = p.C0 + p.C1;
+  const int cblocks = Cin / KT;
+  const int nk0 = p.ksize * p.ksize * cblocks;
+  const int Csc_all = p.Csc + p.Csc1;
+  const int nk = nk0 + (p.sc_src ? Csc_all / KT : 0);
+  const int K1 = p.ksize * p.ksize * Cin;
+  const int half = p.ksize >> 1;
+
+  const int ch = tid & 7;  // A: fp32 elements 4ch..4ch+3 of the K-tile; B: 16-B chunk ch of the split row
+  int a_b[A_LD], a_h[A_LD], a_w[A_LD];
+  bool a_ok[A_LD];
+#pragma unroll
+  for (int i = 0; i < A_LD; ++i) {
+    const int r = (tid >> 3) + i * ROWS_PER_PASS;
+    const int m = m0 + r;
+    a_ok[i] = (r < BM) && (m < p.M);
+    const int mm = a_ok[i] ? m : 0;
+    a_b[i] = mm / HW;
+    const int rem = mm - a_b[i] * HW;
+    a_h[i] = rem / p.W;
+    a_w[i] = rem - a_h[i] * p.W;
+  }
+
+  u32x4 ra[A_LD], rb[B_LD];
+  auto gload = [&](int kt) {
+    const float* src;
+    int cs, cc, dy, dx;
+    const bf16_t* wbase;
+    int wld;
+    if (kt < nk0) {
+      const int tap = kt / cblocks;
+      const int c = (kt - tap * cblocks) * KT;
+      dy = tap / p.ksize - half;
+      dx = tap % p.ksize - half;
+      if (c < p.C0) { src = (const float*)p.src0; cs = p.C0; cc = c; }
+      else { src = (const float*)p.src1; cs = p.C1; cc = c - p.C0; }
+      wbase = (const bf16_t*)p.wgt + 2 * (tap * Cin + c);
+      wld = 2 * K1;
+    } else {
+      const int c = (kt - nk0) * KT;
+      if (c < p.Csc) { src = (const float*)p.sc_src; cs = p.Csc; cc = c; }
+      else { src = (const float*)p.sc_src1; cs = p.Csc1; cc = c - p.Csc; }
+      dy = 0; dx = 0;
+      wbase = (const bf16_t*)p.sc_wgt + 2 * c;
+      wld = 2 * Csc_all;
+    }
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int hh = a_h[i] + dy, ww = a_w[i] + dx;
+      const bool ok = a_ok[i] && hh >= 0 && hh < p.H && ww >= 0 && ww < p.W;
+      if (ok) ra[i] = *(const u32x4*)(src + ((size_t)(a_b[i] * p.H + hh) * p.W + ww) * cs + cc + ch * 4);
+      else ra[i] = u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      const int r = (tid >> 3) + i * ROWS_PER_PASS;
+      if (r < BN) rb[i] = *(const u32x4*)(wbase + (size_t)(n0 + r) * wld + ch * 8);
+    }
+  };
+  // A: 4 fp32 -> 4 hi bf16 (8 B, hi half) + 4 lo bf16 (8 B, lo half); B: the pre-split chunk as is
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A_LD; ++i) {
+      const int r = (tid >> 3) + i * ROWS_PER_PASS;
+      if (r < BM) {
+        const u32x4 v = ra[i];
+        const uint32_t h01 = pack_bf16x2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+        const uint32_t h23 = pack_bf16x2(__uint_as_float(v[2]), __uint_as_float(v[3]));
+        const uint32_t l01 = pack_bf16x2(__uint_as_float(v[0]) - __uint_as_float(h01 << 16),
+                                         __uint_as_float(v[1]) - __uint_as_float(h01 & 0xffff0000u));
+        const uint32_t l23 = pack_bf16x2(__uint_as_float(v[2]) - __uint_as_float(h23 << 16),
+                                         __uint_as_float(v[3]) - __uint_as_float(h23 & 0xffff0000u));
+        typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+        *(u32x2*)(AS(buf) + swz(r, ch >> 1) + (ch & 1) * 8) = u32x2{h01, h23};
+        *(u32x2*)(AS(buf) + swz(r, 4 + (ch >> 1)) + (ch & 1) * 8) = u32x2{l01, l23};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_LD; ++i) {
+      const int r = (tid >> 3) + i * ROWS_PER_PASS;
+      if (r < BN) *(u32x4*)(BS(buf) + swz(r, ch)) = rb[i];
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int kb = (int)((long long)ks * nk / p.ksplit), ke = (int)((long long)(ks + 1) * nk / p.ksplit);
+  gload(kb);
+  lstore(0);
+  __syncthreads();
+
+  const int lrow = lane & 15;
+  const int lg = lane >> 4;
+  for (int kt = kb; kt < ke; ++kt) {
+    const int cur = (kt - kb) & 1;
+    if (kt + 1 < ke) gload(kt + 1);
+    u32x4 ah[FM], al[FM], bh[FN], bl[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      ah[i] = *(const u32x4*)(AS(cur) + swz(wm * TM + i * 16 + lrow, lg));
+      al[i] = *(const u32x4*)(AS(cur) + swz(wm * TM + i * 16 + lrow, 4 + lg));
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      bh[j] = *(const u32x4*)(BS(cur) + swz(wn * TN + j * 16 + lrow, lg));
+      bl[j] = *(const u32x4*)(BS(cur) + swz(wn * TN + j * 16 + lrow, 4 + lg));
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        acc[i][j] = mfma_chunk<bf16_t>(ah[i], bh[j], acc[i][j]);
+        acc[i][j] = mfma_chunk<bf16_t>(ah[i], bl[j], acc[i][j]);
+        acc[i][j] = mfma_chunk<bf16_t>(al[i], bh[j], acc[i][j]);
+      }
+    if (kt + 1 < ke) lstore(cur ^ 1);
+    __syncthreads();
+  }
+#undef AS
+#undef BS
+  if (p.ksplit > 1) {
+    float* const wsp = p.ws + (size_t)ks * p.M * p.Cout;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm * TM + i * 16 + lg * 4 + e;
+        if (m < p.M) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) wsp[(size_t)m * p.Cout + n0 + wn * TN + j * 16 + lrow] = acc[i][j][e];
+        }
+      }
+    return;
+  }
+  if constexpr (TM == 64 && TN == 64) {
+    // LDS-staged epilogue: 16-B output stores, one statistics atomic pair per channel per block
+    const int b_lo = m0 / HW, b_hi = (min(m0 + BM, p.M) - 1) / HW;
+    epilogue_lds<float, WM, BN>(p, acc, m0 + wm * TM, n0 + wn * TN, lane, (float*)(smem + wid * (64 * 68 * 4)),
+                                (float*)(smem + WM * WN * (64 * 68 * 4)), wm, b_lo == b_hi ? b_lo : -1, n0);
+  } else {
+    epilogue<float, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, lane);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // v2 (bf16): 8 waves, 64x64 wave tiles, operands streamed global->LDS by buffer_load...lds
 // (LDS-DMA, no VGPR staging), 3-stage ring with counted vmcnt + raw s_barrier so two
 // K-tiles stay in flight across the barrier.  Zero padding of the 3x3 halo comes from the
@@ -1196,6 +1382,30 @@ int launch_conv(ConvParams p, int npad, hipStream_t s, snrse_ctx& cx) {
   return (int)hipGetLastError();
 }
 
+template <int BM, int BN, int WM, int WN>
+int launch_x3(ConvParams p, hipStream_t s, snrse_ctx& cx) {
+  constexpr size_t main_lds = (size_t)2 * (BM + BN) * 128;
+  constexpr size_t epi_lds = (BM / WM == 64 && BN / WN == 64) ? (size_t)WM * WN * 64 * 68 * 4 + WM * BN * 2 * 4 : 0;
+  constexpr size_t lds = main_lds > epi_lds ? main_lds : epi_lds;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_x3_kernel<BM, BN, WM, WN>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  SNRSE_RET(attr);
+  p.ntn = p.Cout / BN;
+  const int tiles = ((p.M + BM - 1) / BM) * p.ntn;
+  const int nk = p.ksize * p.ksize * ((p.C0 + p.C1) / 32) + (p.sc_src ? (p.Csc + p.Csc1) / 32 : 0);
+  p.ksplit = choose_ksplit(p, tiles, nk, cx, 2);
+  p.ws = cx.ws;
+  cx.last_ksplit = p.ksplit;
+  hipLaunchKernelGGL((conv_x3_kernel<BM, BN, WM, WN>), dim3(tiles * p.ksplit), dim3(64 * WM * WN), lds, s, p);
+  if (p.ksplit > 1) {
+    SNRSE_LAUNCH_CHECK();
+    const int HW = p.H * p.W, ppb = 64;
+    hipLaunchKernelGGL((conv_splitk_finalize<float>), dim3(p.B * ((HW + ppb - 1) / ppb), p.Cout / 128), dim3(256), 0, s,
+                       p, ppb);
+  }
+  return (int)hipGetLastError();
+}
+
 template <int BM, int BN, typename TO>
 int launch_glds(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   constexpr size_t lds = (size_t)3 * (BM + BN) * 128;
@@ -1273,6 +1483,12 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
   using TrB = ConvTraits<bf16_t>;
   using TrF = ConvTraits<float>;
   snrse_ctx& cx = *snrse_ctx_resolve(ctx);
+  // SNRSE_F32X3: fp32 activations / output, weights pre-split into bf16 hi / lo rows (conv_x3_kernel)
+  const bool x3 = dtype == SNRSE_F32X3;
+  if (x3) {
+    if (Cout < 128 || Cout % 128 || gn_scale || out_f32) return SNRSE_EINVAL;
+    dtype = SNRSE_F32;
+  }
   const int KT = dtype == SNRSE_BF16 ? TrB::KT : TrF::KT;
   if (!src0 || !wgt || !out || (ksize != 1 && ksize != 3)) return SNRSE_EINVAL;
   if (C0 % KT || C1 % KT || (sc_src && (Csc % KT || Csc1 % KT))) return SNRSE_EINVAL;
@@ -1309,6 +1525,12 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
   if (stats && !cx.stats_zeroed) SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * Cout, stream));
   if (dtype != SNRSE_BF16 && dtype != SNRSE_F32) return SNRSE_EINVAL;
   auto run = [&](const ConvParams& q) {
+    if (x3) {
+      cx.last_kernel = 3;
+      if (cx.x3_tile == 2) return launch_x3<256, 128, 4, 2>(q, stream, cx);
+      if (cx.x3_tile == 3 && q.Cout % 256 == 0) return launch_x3<128, 256, 2, 4>(q, stream, cx);
+      return launch_x3<128, 128, 2, 2>(q, stream, cx);
+    }
     if (dtype == SNRSE_BF16)
       return out_f32 ? dispatch_conv<bf16_t, float>(q, stream, cx) : dispatch_conv<bf16_t, bf16_t>(q, stream, cx);
     return dispatch_conv<float, float>(q, stream, cx);

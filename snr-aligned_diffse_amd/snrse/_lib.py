@@ -16,7 +16,7 @@ import torch  # noqa: F401
 
 from .build import LIB
 
-F32, BF16, F16, F64 = 0, 1, 2, 3
+F32, BF16, F16, F64, F32X3 = 0, 1, 2, 3, 4
 
 _vp, _i, _f, _u64, _ll = C.c_void_p, C.c_int, C.c_float, C.c_uint64, C.c_longlong
 

@@ -115,10 +115,16 @@ def _pack1x1(w, dt, npad=None):
 class NCSNppHIP:
     """Device-resident packed weights + the forward executor."""
 
-    def __init__(self, sd: dict, dtype=torch.bfloat16, device="cuda", **cfg):
+    def __init__(self, sd: dict, dtype=torch.bfloat16, device="cuda", gemm="exact", **cfg):
+        """gemm (fp32 only): "exact" = v_mfma_f32_16x16x4_f32 GEMMs; "x3" = the split-bf16 GEMM
+        (ops.split_weight, three bf16 products per K-tile) for the ResBlock and input convs, exact fp32
+        for the attention projections and the pyramid heads."""
         if not torch.cuda.is_available():
             raise RuntimeError("snrse: NCSNppHIP needs a HIP device (no CPU fallback)")
+        if gemm not in ("exact", "x3") or (gemm == "x3" and dtype != torch.float32):
+            raise ValueError(f"snrse: gemm={gemm!r} with dtype {dtype} (x3 is an fp32 mode)")
         self.dtype = dtype
+        self.gemm = gemm
         self.device = torch.device(device)
         self._arena = None  # ops.StatsArena of the GroupNorm statistics, one fill per evaluation
         self._arenas = {}   # one arena per launch stream (the two-stream sampler runs evaluations concurrently)
@@ -176,6 +182,14 @@ class NCSNppHIP:
             self.mw[m.idx] = e
         W["dense_w"] = torch.cat(dense_w, 0).contiguous()
         W["dense_b"] = torch.cat(dense_b, 0).contiguous()
+        if gemm == "x3":
+            W["in_w"] = ops.split_weight(W["in_w"])
+            for m in self.plan:
+                if m.kind == "rb":
+                    e = self.mw[m.idx]
+                    for k in ("w0", "w1", "w2"):
+                        if k in e:
+                            e[k] = ops.split_weight(e[k])
 
     # ------------------------------------------------------------------ blocks
     # Every activation travels with its per-channel GroupNorm statistics, produced by the

@@ -30,6 +30,28 @@ F32, BF16 = _lib.F32, _lib.BF16
 INV_SQRT2 = 1.0 / math.sqrt(2.0)
 
 
+def conv_code(act_dtype: torch.dtype, wgt_dtype: torch.dtype) -> int:
+    """snrse_conv2d dtype: fp32 activations with bf16 weights are the split-bf16 fp32 GEMM (weights from
+    split_weight), else the activations' dtype (weights of the same dtype)."""
+    if act_dtype == torch.float32 and wgt_dtype == torch.bfloat16:
+        return _lib.F32X3
+    if wgt_dtype != act_dtype:
+        raise TypeError(f"snrse: conv weights {wgt_dtype} for {act_dtype} activations")
+    return code(act_dtype)
+
+
+def split_weight(w: torch.Tensor) -> torch.Tensor:
+    """fp32 packed conv weights [N][K] (K % 32 == 0) -> the SNRSE_F32X3 layout [N][2K] bf16: per 32-element
+    K-tile, 32 hi = bf16(w) then 32 lo = bf16(w - hi)."""
+    n, k = w.shape
+    if k % 32:
+        raise ValueError(f"snrse: split weights need K % 32 == 0, got {k}")
+    w = w.float().reshape(n, k // 32, 1, 32)
+    hi = w.to(torch.bfloat16)
+    lo = (w - hi.float()).to(torch.bfloat16)
+    return torch.cat([hi, lo], 2).reshape(n, 2 * k).contiguous()
+
+
 def code(dtype: torch.dtype) -> int:
     if dtype == torch.float32:
         return F32
@@ -149,6 +171,8 @@ def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_w
     Csc = 0 if sc is None else sc.shape[3]
     Csc1 = 0 if sc1 is None else sc1.shape[3]
     odt = torch.float32 if out_f32 else src0.dtype
+    if sc_wgt is not None and sc_wgt.dtype != wgt.dtype:
+        raise TypeError("snrse: conv2d wgt and sc_wgt must share one layout (both split or neither)")
     if out is None:
         out = torch.empty(B, H, W, cout, device=src0.device, dtype=odt)
     _stats_zeroed(cx, stats)
@@ -157,7 +181,7 @@ def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_w
               0 if temb is None else temb.shape[1], _ptr(res), 0 if res is None else res.shape[-1], float(out_scale), _ptr(comb),
               _ptr(comb_w), _ptr(comb_b), out.data_ptr(), cout, out.shape[-1], _ptr(stats),
               None if gn is None else gn[0].data_ptr(), None if gn is None else gn[1].data_ptr(), int(bool(gn_act)),
-              code(src0.dtype), int(out_f32), _stream())
+              conv_code(src0.dtype, wgt.dtype), int(out_f32), _stream())
     return out
 
 
@@ -202,7 +226,8 @@ def probe_read(max_calls, dev=None, all_threads=False):
     return out_ms, out_k
 
 
-KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 5: "conv_halo5_kernel", 10: "conv_head_kernel"}
+KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 3: "conv_x3_kernel", 5: "conv_halo5_kernel",
+           10: "conv_head_kernel"}
 
 
 def kernel_name(gen):

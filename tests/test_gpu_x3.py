@@ -1,0 +1,130 @@
+"""Parity of the split-bf16 fp32 GEMM (snrse_conv2d dtype SNRSE_F32X3, conv_x3_kernel): fp32
+activations, weights pre-split by ops.split_weight, three bf16 MFMA products per K-tile.
+
+Tolerances: single convs 3e-5 relative RMS against a float64 torch conv of the same fp32 operands
+(the split keeps ~16 significant bits of each operand: ~2^-16 relative per product, averaging down
+over K); the network and the N=5 PC loop are held to the north star's 1e-4 absolute RMS on the
+complex spectrogram against the reference goldens (CPU emulation of this arithmetic on the PC golden:
+6.0e-5, tools/x3_emulate.py)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import fnormal, formula_sd, golden
+from test_gpu_kernels import abs_rms, nchw, nhwc, rel
+
+pytestmark = pytest.mark.gpu
+TOL = 3e-5
+
+
+@pytest.mark.parametrize("shape", [(2, 128, 128, 8, 16), (1, 256, 128, 4, 8), (3, 128, 256, 5, 7), (2, 384, 256, 4, 4),
+                                   (2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (1, 256, 256, 12, 64),
+                                   (2, 64, 128, 16, 32)])
+def test_x3_conv3x3(gpu, shape):
+    from snrse import ops
+    B, cin, cout, H, W = shape
+    x = torch.from_numpy(fnormal("t.conv.x", (B, cin, H, W)))
+    w = torch.from_numpy(fnormal("t.conv.w", (cout, cin, 3, 3))) / math.sqrt(9 * cin)
+    b = torch.from_numpy(fnormal("t.conv.b", (cout,)))
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1)
+    c0 = 256 if cin == 384 else cin
+    xg = nhwc(x).to(gpu)
+    src0, src1 = (xg[..., :c0].contiguous(), xg[..., c0:].contiguous()) if c0 != cin else (xg, None)
+    wp = ops.split_weight(w.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu))
+    assert wp.dtype == torch.bfloat16 and wp.shape == (cout, 2 * 9 * cin)
+    out = ops.conv2d(src0, wp, 3, cout, bias=b.to(gpu), src1=src1)
+    assert ops.get_option("last_kernel") == 3
+    assert out.dtype == torch.float32
+    assert rel(nchw(out), ref) < TOL
+
+
+@pytest.mark.parametrize("hw", [(8, 8), (8, 64), (64, 128)])
+def test_x3_epilogue_shortcut_temb_comb(gpu, hw):
+    """Conv_1 + Conv_2 shortcut (split weights) as extra K, temb, residual scale, Combine, stats; the
+    small shapes run split-K (conv_splitk_finalize), the 64 x 128 one (256 tiles) the in-kernel LDS epilogue."""
+    from snrse import ops
+    B, cin, cout = 2, 128, 256
+    H, W = hw
+    h = torch.from_numpy(fnormal("t.ep.h", (B, cout, H, W)))
+    xs = torch.from_numpy(fnormal("t.ep.xs", (B, cin, H, W)))
+    w1 = torch.from_numpy(fnormal("t.ep.w1", (cout, cout, 3, 3))) / 48
+    w2 = torch.from_numpy(fnormal("t.ep.w2", (cout, cin, 1, 1))) / 11
+    b1 = torch.from_numpy(fnormal("t.ep.b1", (cout,)))
+    temb = torch.from_numpy(fnormal("t.ep.temb", (B, 300)))
+    pyr = torch.from_numpy(fnormal("t.ep.pyr", (B, 4, H, W)))
+    cw = torch.from_numpy(fnormal("t.ep.cw", (cout, 4)))
+    cb = torch.from_numpy(fnormal("t.ep.cb", (cout,)))
+    ref = (F.conv2d(h.double(), w1.double(), b1.double(), padding=1) + F.conv2d(xs.double(), w2.double())
+           + temb[:, 20:20 + cout, None, None].double()) / math.sqrt(2)
+    ref = ref + torch.einsum("bihw,oi->bohw", pyr.double(), cw.double()) + cb.double()[None, :, None, None]
+    st = ops.new_stats(B, cout)
+    out = ops.conv2d(nhwc(h).to(gpu), ops.split_weight(w1.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu)),
+                     3, cout, bias=b1.to(gpu), sc=nhwc(xs).to(gpu),
+                     sc_wgt=ops.split_weight(w2.reshape(cout, cin).to(gpu)), temb=temb.to(gpu), temb_off=20,
+                     out_scale=1 / math.sqrt(2), comb=nhwc(pyr).to(gpu), comb_w=cw.to(gpu), comb_b=cb.to(gpu),
+                     stats=st)
+    ksplit = ops.get_option("last_ksplit")
+    assert (ksplit > 1) == (H * W <= 512), ksplit  # 2 / 16 output tiles split K; 256 tiles do not
+    assert rel(nchw(out), ref) < TOL
+    o = out.double()
+    st_ref = torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)
+    assert rel(ops.fold_stats(st), st_ref) < 1e-5
+
+
+def test_x3_residual_and_layout_errors(gpu):
+    from snrse import ops
+    B, C, H, W = 1, 128, 8, 64
+    x = torch.from_numpy(fnormal("t.x3r.x", (B, C, H, W)))
+    r = torch.from_numpy(fnormal("t.x3r.r", (B, C, H, W)))
+    w = torch.from_numpy(fnormal("t.x3r.w", (C, C, 1, 1))) / 11
+    ref = (F.conv2d(x.double(), w.double()) + r.double()) * 0.5
+    wp = w.reshape(C, C).to(gpu)
+    out = ops.conv2d(nhwc(x).to(gpu), ops.split_weight(wp), 1, C, res=nhwc(r).to(gpu), out_scale=0.5)
+    assert rel(nchw(out), ref) < TOL
+    with pytest.raises(TypeError):  # split main weights with exact shortcut weights
+        ops.conv2d(nhwc(x).to(gpu), ops.split_weight(wp), 1, C, sc=nhwc(x).to(gpu), sc_wgt=wp)
+    with pytest.raises(RuntimeError):  # Cout < 128 has no split kernel (the pyramid heads stay exact fp32)
+        ops.conv2d(nhwc(x).to(gpu), ops.split_weight(torch.zeros(16, 9 * C, device=gpu)), 3, 4)
+
+
+def test_x3_level0_vs_exact_fp32(gpu):
+    """One C2 level-0 shape (256 x 512, 128 -> 128) on two images: split vs the exact-fp32 kernel."""
+    from snrse import ops
+    B, C, H, W = 2, 128, 256, 512
+    g = torch.Generator(device=gpu).manual_seed(3)
+    x = torch.randn(B, H, W, C, device=gpu, generator=g)
+    w = torch.randn(C, 9 * C, device=gpu, generator=g) / math.sqrt(9 * C)
+    b = torch.randn(C, device=gpu, generator=g)
+    st_a, st_b = ops.new_stats(B, C), ops.new_stats(B, C)
+    a = ops.conv2d(x, w, 3, C, bias=b, stats=st_a)
+    assert ops.get_option("last_kernel") == 1
+    s = ops.conv2d(x, ops.split_weight(w), 3, C, bias=b, stats=st_b)
+    assert ops.get_option("last_kernel") == 3
+    assert rel(s, a) < TOL
+    assert rel(ops.fold_stats(st_b), ops.fold_stats(st_a)) < 1e-5
+
+
+@pytest.fixture(scope="module")
+def net_x3(gpu):
+    from snrse import ncsnpp
+    sd = {k: torch.from_numpy(v) for k, v in formula_sd("ncsnpp").items()}
+    return ncsnpp.NCSNppHIP(sd, dtype=torch.float32, device=gpu, gemm="x3")
+
+
+def test_x3_ncsnpp_full_golden(gpu, net_x3):
+    g = golden("ncsnpp_full.npz")
+    x = torch.from_numpy(fnormal("golden.ncsnpp.x", (2, 2, 256, 64), complex_=True)) * 0.5
+    t = torch.tensor([0.5, 0.8], device=gpu)
+    out = net_x3.dnn(x[:, 0].contiguous().to(gpu), x[:, 1].contiguous().to(gpu), t)
+    assert rel(out, g["out"][:, 0]) < 1e-4
+    assert abs_rms(out, g["out"][:, 0]) < 1e-4
+
+
+def test_x3_pc_loop_vs_reference_golden(gpu, net_x3):
+    """The benched class (PCEnhancer) in the fp32x3 mode on the reference's N=5 OUVE run."""
+    import paritycheck
+    r = paritycheck.pc_vs_golden(gpu, net_x3)
+    assert r["dtype"] == "fp32x3" and r["nfe"] == 10
+    assert r["abs_rms"] < 1e-4, r

@@ -34,3 +34,18 @@ def test_training_api_surface_and_unsupported_branches():
     x = torch.zeros(1, 1, 256, 64, dtype=torch.complex64)
     with pytest.raises(NotImplementedError):
         m._step((x, x), 0)
+
+
+def test_split_weight_layout():
+    """ops.split_weight (the SNRSE_F32X3 weight layout): per 32-element K-tile 32 hi then 32 lo bf16,
+    hi + lo within 2^-16 of the fp32 weight."""
+    import torch
+    from snrse import ops
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(3, 96, generator=g) * torch.logspace(-3, 3, 96)
+    s = ops.split_weight(w)
+    assert s.dtype == torch.bfloat16 and s.shape == (3, 192)
+    t = s.float().reshape(3, 3, 2, 32)
+    hi, lo = t[:, :, 0].reshape(3, 96), t[:, :, 1].reshape(3, 96)
+    assert torch.equal(hi, w.to(torch.bfloat16).float())
+    assert ((hi + lo - w).abs() <= w.abs() * 2.0 ** -16).all()
