@@ -752,6 +752,206 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvParams p) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Halo form of the split-bf16 fp32 GEMM (3x3, H % 4 == 0, W % 64 == 0): the register-staged kernel
+// above re-reads every input pixel from L2 once per tap (9x); here a workgroup owns a 4-row x 64-px
+// output tile x 128 couts and stages, per 32-channel chunk, the tile's (4+2) x (64+2) halo ONCE in
+// LDS as split hi / lo bf16 rows (128 B: hi chunks 0-3, lo chunks 4-7, swz() layout), double
+// buffered so chunk c+1's halo is fetched into registers during chunk c's first tap and stored after
+// its second -- no barrier of its own.  Weights run through a 3-slot ring of one tap each (128 couts x
+// 128 B of pre-split rows = 16 KB, LDS-DMA with the swizzle applied on the source chunk), issued two
+// taps ahead.  8 waves: wave w computes image row w & 3 (64 px) x couts (w >> 2) * 64 .. + 63, i.e.
+// 4 x 4 fragments x 3 MFMAs per tap.  Shortcut K (the fused 1x1 Conv_2) runs as chunks of one (center)
+// tap over the shortcut source's halo.  LDS: 2 x 50.7 KB halo + 48 KB ring = 147 KB, one workgroup per
+// CU (2 waves per SIMD); the epilogue reuses it as the per-wave staging of epilogue_lds.
+namespace x3h {
+constexpr int TH = 4, TW = 64, HC = TW + 2, HROWS = (TH + 2) * HC;  // 396 halo rows
+constexpr int HBYTES = HROWS * 128;                                 // 50,688
+constexpr int HJ = (HROWS * 8 + 511) / 512;                         // 16-B halo loads per thread: 7
+constexpr int TAPB = 128 * 128;                                     // one tap's weights: 16 KB
+constexpr size_t LDS_MAIN = 2 * (size_t)HBYTES + 3 * (size_t)TAPB;
+constexpr size_t LDS_EPI = 8 * (64 * 68 * 4) + 4 * 128 * 2 * 4;
+constexpr size_t LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
+}  // namespace x3h
+
+// s_waitcnt vmcnt(n) for the counts the x3h schedule produces (anything else waits for all)
+SNRSE_DEV void x3h_vm_wait(int n) {
+  switch (n) {
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+__global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
+  using namespace x3h;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const ring = smem + 2 * HBYTES;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid & 3, wc = wid >> 2;
+  const int nb = gridDim.x, bid = blockIdx.x;
+  const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7, pos = bid >> 3;
+  const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
+  const int n0 = (g % p.ntn) * 128;
+  int tile = g / p.ntn;
+  const int ntw = p.W / TW, nth = p.H / TH;
+  const int w0 = (tile % ntw) * TW;
+  tile /= ntw;
+  const int h0 = (tile % nth) * TH;
+  const int bb = tile / nth;
+
+  const int Cin = p.C0 + p.C1;
+  const int cbm = Cin / 32;
+  const int Csc_all = p.Csc + p.Csc1;
+  const int cbs = p.sc_src ? Csc_all / 32 : 0;
+  const int ncb = cbm + cbs;
+  const int nq = 9 * cbm + cbs;
+  const int K1 = 9 * Cin;
+
+  // this thread's halo pieces: halo row (tid + 512 j) >> 3, 16-B fp32 chunk tid & 7 (4 channels)
+  const int hch = tid & 7;
+  int hpix[HJ];
+  bool hok[HJ];
+#pragma unroll
+  for (int j = 0; j < HJ; ++j) {
+    const int hr = (tid + 512 * j) >> 3;
+    const int hy = hr / HC, hx = hr - hy * HC;
+    const int ih = h0 + hy - 1, iw = w0 + hx - 1;
+    hok[j] = hr < HROWS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+    hpix[j] = (bb * p.H + ih) * p.W + iw;
+  }
+  u32x4 hv[HJ];
+  auto halo_load = [&](int c) {
+    const void* base;
+    long long bytes;
+    int cs, cc;
+    if (c < cbm) {
+      const int ch = c * 32;
+      if (ch < p.C0) { base = p.src0; bytes = p.bytes0; cs = p.C0; cc = ch; }
+      else { base = p.src1; bytes = p.bytes1; cs = p.C1; cc = ch - p.C0; }
+    } else {
+      const int ch = (c - cbm) * 32;
+      if (ch < p.Csc) { base = p.sc_src; bytes = p.sc_bytes0; cs = p.Csc; cc = ch; }
+      else { base = p.sc_src1; bytes = p.sc_bytes1; cs = p.Csc1; cc = ch - p.Csc; }
+    }
+    const __amdgpu_buffer_rsrc_t r = make_rsrc(base, bytes);
+#pragma unroll
+    for (int j = 0; j < HJ; ++j) {
+      const int voff = hok[j] ? (hpix[j] * cs + cc + hch * 4) * 4 : (int)0x80000000;  // outside: zero padding
+      hv[j] = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
+    }
+  };
+  typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+  auto halo_store = [&](int buf) {
+    char* const hb = smem + buf * HBYTES;
+#pragma unroll
+    for (int j = 0; j < HJ; ++j) {
+      const int hr = (tid + 512 * j) >> 3;
+      if (j == HJ - 1 && hr >= HROWS) break;
+      const u32x4 v = hv[j];
+      const uint32_t h01 = pack_bf16x2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+      const uint32_t h23 = pack_bf16x2(__uint_as_float(v[2]), __uint_as_float(v[3]));
+      const uint32_t l01 = pack_bf16x2(__uint_as_float(v[0]) - __uint_as_float(h01 << 16),
+                                       __uint_as_float(v[1]) - __uint_as_float(h01 & 0xffff0000u));
+      const uint32_t l23 = pack_bf16x2(__uint_as_float(v[2]) - __uint_as_float(h23 << 16),
+                                       __uint_as_float(v[3]) - __uint_as_float(h23 & 0xffff0000u));
+      *(u32x2*)(hb + swz(hr, hch >> 1) + (hch & 1) * 8) = u32x2{h01, h23};
+      *(u32x2*)(hb + swz(hr, 4 + (hch >> 1)) + (hch & 1) * 8) = u32x2{l01, l23};
+    }
+  };
+  // phase q -> (chunk, tap): main chunks 9 taps each, then the shortcut chunks' center tap
+  auto phase_chunk = [&](int q) { return q < 9 * cbm ? q / 9 : cbm + (q - 9 * cbm); };
+  auto phase_tap = [&](int q) { return q < 9 * cbm ? q - (q / 9) * 9 : 4; };
+  auto first_with_next = [&](int q) {  // phase q starts a chunk that has a successor (its halo prefetch)
+    if (q < 0 || q >= nq) return false;
+    const int c = phase_chunk(q);
+    return (c < cbm ? phase_tap(q) == 0 : true) && c + 1 < ncb;
+  };
+  // weights of phase q -> ring slot q % 3: 16 pieces of 1 KB (8 rows x 128 B), 2 per wave
+  auto wload = [&](int q) {
+    const int c = phase_chunk(q), tp = phase_tap(q);
+    const bool mainw = c < cbm;
+    const int wld = mainw ? 2 * K1 : 2 * Csc_all;                      // bf16 elements per row
+    const int koff = mainw ? 2 * (tp * Cin + c * 32) : 2 * ((c - cbm) * 32);
+    const __amdgpu_buffer_rsrc_t r = mainw ? make_rsrc(p.wgt, p.wbytes) : make_rsrc(p.sc_wgt, p.sc_wbytes);
+    char* dst = ring + (q % 3) * TAPB;
+    const int rl = lane >> 3, sl = lane & 7;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int pc = wid * 2 + k;
+      const int row = pc * 8 + rl;
+      const unsigned voff = (unsigned)(((n0 + row) * wld + koff + (sl ^ (row & 7)) * 8) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(dst + pc * 1024), 16,
+                                               voff, 0, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  wload(0);
+  if (nq > 1) wload(1);
+  halo_load(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  halo_store(0);
+  const int lrow = lane & 15, lg = lane >> 4;
+  for (int q = 0; q < nq; ++q) {
+    const int c = phase_chunk(q), tp = phase_tap(q);
+    // DMA(q) done: wait for all but the ops issued after it (see the schedule in the header comment)
+    x3h_vm_wait(7 * (int)first_with_next(q - 2) + 2 * (int)(q + 1 < nq) + 7 * (int)first_with_next(q - 1));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (q + 2 < nq) wload(q + 2);
+    const bool pre = first_with_next(q);
+    if (pre) halo_load(c + 1);
+    const char* hb = smem + (c & 1) * HBYTES;
+    const char* sb = ring + (q % 3) * TAPB;
+    const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
+    const int hbase = (wr + dy + 1) * HC + dx + 1 + lrow;
+    u32x4 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ah[i] = *(const u32x4*)(hb + swz(hbase + 16 * i, lg));
+      al[i] = *(const u32x4*)(hb + swz(hbase + 16 * i, 4 + lg));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bh[j] = *(const u32x4*)(sb + swz(wc * 64 + j * 16 + lrow, lg));
+      bl[j] = *(const u32x4*)(sb + swz(wc * 64 + j * 16 + lrow, 4 + lg));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j] = mfma_chunk<bf16_t>(ah[i], bh[j], acc[i][j]);
+        acc[i][j] = mfma_chunk<bf16_t>(ah[i], bl[j], acc[i][j]);
+        acc[i][j] = mfma_chunk<bf16_t>(al[i], bh[j], acc[i][j]);
+      }
+    // the next chunk's halo goes to the other buffer after this chunk's second tap (its first and only
+    // one for a shortcut chunk); only the DMAs issued since the halo loads may still be in flight
+    const int q0 = q < 9 * cbm ? q - tp : q;  // first phase of this chunk
+    const bool last_of_chunk = c < cbm ? tp == 8 : true;
+    const bool store_now = c + 1 < ncb && (c < cbm ? tp == 1 : true);
+    if (store_now) {
+      x3h_vm_wait(q == q0 ? 0 : 2 * (int)(q0 + 3 < nq));
+      halo_store((c + 1) & 1);
+    }
+    (void)last_of_chunk;
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // LDS is reused as the epilogue staging area
+  const int mb = (bb * p.H + h0 + wr) * p.W + w0;
+  epilogue_lds<float, 4, 128>(p, acc, mb, n0 + wc * 64, lane, (float*)(smem + wid * (64 * 68 * 4)),
+                              (float*)(smem + 8 * (64 * 68 * 4)), wr, bb, n0);
+}
+
+// ---------------------------------------------------------------------------------------
 // v2 (bf16): 8 waves, 64x64 wave tiles, operands streamed global->LDS by buffer_load...lds
 // (LDS-DMA, no VGPR staging), 3-stage ring with counted vmcnt + raw s_barrier so two
 // K-tiles stay in flight across the barrier.  Zero padding of the 3x3 halo comes from the
@@ -1406,6 +1606,16 @@ int launch_x3(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   return (int)hipGetLastError();
 }
 
+int launch_x3h(ConvParams p, hipStream_t s, int tiles) {
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_x3h_kernel,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)x3h::LDS);
+  SNRSE_RET(attr);
+  p.ntn = p.Cout / 128;
+  p.ksplit = 1;
+  hipLaunchKernelGGL(conv_x3h_kernel, dim3(tiles), dim3(512), x3h::LDS, s, p);
+  return (int)hipGetLastError();
+}
+
 template <int BM, int BN, typename TO>
 int launch_glds(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   constexpr size_t lds = (size_t)3 * (BM + BN) * 128;
@@ -1526,6 +1736,13 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
   if (dtype != SNRSE_BF16 && dtype != SNRSE_F32) return SNRSE_EINVAL;
   auto run = [&](const ConvParams& q) {
     if (x3) {
+      const int x3h_tiles = q.B * (q.H / x3h::TH) * (q.W / x3h::TW) * (q.Cout / 128);
+      const bool x3h_ok = q.ksize == 3 && q.H % x3h::TH == 0 && q.W % x3h::TW == 0;
+      if (x3h_ok && ((cx.x3_tile == 0 && x3h_tiles >= 256) || cx.x3_tile == 4)) {
+        cx.last_kernel = 4;
+        cx.last_ksplit = 1;
+        return launch_x3h(q, stream, x3h_tiles);
+      }
       cx.last_kernel = 3;
       if (cx.x3_tile == 2) return launch_x3<256, 128, 4, 2>(q, stream, cx);
       if (cx.x3_tile == 3 && q.Cout % 256 == 0) return launch_x3<128, 256, 2, 4>(q, stream, cx);

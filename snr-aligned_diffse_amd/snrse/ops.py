@@ -226,7 +226,8 @@ def probe_read(max_calls, dev=None, all_threads=False):
     return out_ms, out_k
 
 
-KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 3: "conv_x3_kernel", 5: "conv_halo5_kernel",
+KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 3: "conv_x3_kernel", 4: "conv_x3h_kernel",
+           5: "conv_halo5_kernel",
            10: "conv_head_kernel"}
 
 

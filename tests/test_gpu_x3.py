@@ -22,7 +22,10 @@ TOL = 3e-5
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 16), (1, 256, 128, 4, 8), (3, 128, 256, 5, 7), (2, 384, 256, 4, 4),
                                    (2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (1, 256, 256, 12, 64),
                                    (2, 64, 128, 16, 32)])
-def test_x3_conv3x3(gpu, shape):
+@pytest.mark.parametrize("tile", [0, 4])
+def test_x3_conv3x3(gpu, shape, tile):
+    """tile: option x3_tile 0 auto (register-staged at these small grids), 4 the halo kernel where
+    H % 4 == 0 and W % 64 == 0 (else still register-staged)."""
     from snrse import ops
     B, cin, cout, H, W = shape
     x = torch.from_numpy(fnormal("t.conv.x", (B, cin, H, W)))
@@ -34,14 +37,20 @@ def test_x3_conv3x3(gpu, shape):
     src0, src1 = (xg[..., :c0].contiguous(), xg[..., c0:].contiguous()) if c0 != cin else (xg, None)
     wp = ops.split_weight(w.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu))
     assert wp.dtype == torch.bfloat16 and wp.shape == (cout, 2 * 9 * cin)
-    out = ops.conv2d(src0, wp, 3, cout, bias=b.to(gpu), src1=src1)
-    assert ops.get_option("last_kernel") == 3
+    ops.set_option("x3_tile", tile)
+    try:
+        out = ops.conv2d(src0, wp, 3, cout, bias=b.to(gpu), src1=src1)
+        kern = ops.get_option("last_kernel")
+    finally:
+        ops.set_option("x3_tile", 0)
+    assert kern == (4 if tile == 4 and H % 4 == 0 and W % 64 == 0 else 3), kern
     assert out.dtype == torch.float32
     assert rel(nchw(out), ref) < TOL
 
 
+@pytest.mark.parametrize("tile", [0, 4])
 @pytest.mark.parametrize("hw", [(8, 8), (8, 64), (64, 128)])
-def test_x3_epilogue_shortcut_temb_comb(gpu, hw):
+def test_x3_epilogue_shortcut_temb_comb(gpu, hw, tile):
     """Conv_1 + Conv_2 shortcut (split weights) as extra K, temb, residual scale, Combine, stats; the
     small shapes run split-K (conv_splitk_finalize), the 64 x 128 one (256 tiles) the in-kernel LDS epilogue."""
     from snrse import ops
@@ -60,13 +69,20 @@ def test_x3_epilogue_shortcut_temb_comb(gpu, hw):
            + temb[:, 20:20 + cout, None, None].double()) / math.sqrt(2)
     ref = ref + torch.einsum("bihw,oi->bohw", pyr.double(), cw.double()) + cb.double()[None, :, None, None]
     st = ops.new_stats(B, cout)
-    out = ops.conv2d(nhwc(h).to(gpu), ops.split_weight(w1.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu)),
-                     3, cout, bias=b1.to(gpu), sc=nhwc(xs).to(gpu),
-                     sc_wgt=ops.split_weight(w2.reshape(cout, cin).to(gpu)), temb=temb.to(gpu), temb_off=20,
-                     out_scale=1 / math.sqrt(2), comb=nhwc(pyr).to(gpu), comb_w=cw.to(gpu), comb_b=cb.to(gpu),
-                     stats=st)
-    ksplit = ops.get_option("last_ksplit")
-    assert (ksplit > 1) == (H * W <= 512), ksplit  # 2 / 16 output tiles split K; 256 tiles do not
+    ops.set_option("x3_tile", tile)
+    try:
+        out = ops.conv2d(nhwc(h).to(gpu), ops.split_weight(w1.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu)),
+                         3, cout, bias=b1.to(gpu), sc=nhwc(xs).to(gpu),
+                         sc_wgt=ops.split_weight(w2.reshape(cout, cin).to(gpu)), temb=temb.to(gpu), temb_off=20,
+                         out_scale=1 / math.sqrt(2), comb=nhwc(pyr).to(gpu), comb_w=cw.to(gpu), comb_b=cb.to(gpu),
+                         stats=st)
+        kern, ksplit = ops.get_option("last_kernel"), ops.get_option("last_ksplit")
+    finally:
+        ops.set_option("x3_tile", 0)
+    halo = W % 64 == 0 and (tile == 4 or B * (H // 4) * (W // 64) * 2 >= 256)
+    assert kern == (4 if halo else 3), kern
+    if not halo and H * W <= 512:  # 2 / 16 output tiles of the register-staged kernel split K
+        assert ksplit > 1, ksplit
     assert rel(nchw(out), ref) < TOL
     o = out.double()
     st_ref = torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)
@@ -90,7 +106,8 @@ def test_x3_residual_and_layout_errors(gpu):
 
 
 def test_x3_level0_vs_exact_fp32(gpu):
-    """One C2 level-0 shape (256 x 512, 128 -> 128) on two images: split vs the exact-fp32 kernel."""
+    """One C2 level-0 shape (256 x 512, 128 -> 128) on two images: the split halo kernel vs the exact-fp32
+    kernel."""
     from snrse import ops
     B, C, H, W = 2, 128, 256, 512
     g = torch.Generator(device=gpu).manual_seed(3)
@@ -101,7 +118,7 @@ def test_x3_level0_vs_exact_fp32(gpu):
     a = ops.conv2d(x, w, 3, C, bias=b, stats=st_a)
     assert ops.get_option("last_kernel") == 1
     s = ops.conv2d(x, ops.split_weight(w), 3, C, bias=b, stats=st_b)
-    assert ops.get_option("last_kernel") == 3
+    assert ops.get_option("last_kernel") == 4  # 1,024 tiles: the halo kernel
     assert rel(s, a) < TOL
     assert rel(ops.fold_stats(st_b), ops.fold_stats(st_a)) < 1e-5
 

@@ -35,7 +35,7 @@ def time_call(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--tiles", default="1,2,3")
+    ap.add_argument("--tiles", default="0,1,3")
     ap.add_argument("--exact", type=int, default=1)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
