@@ -544,7 +544,12 @@ def run(args):
         # the timed network object itself on the reference's N=5 OUVE PC run (paritycheck.py), after the
         # timed region: pins the benched code's numerics in the same JSON line
         import paritycheck
-        r = paritycheck.pc_vs_golden(dev, net)
+        if args.dtype == "fp32x3":  # the golden's [2, 256, 64] grid is small: force the benched halo kernel
+            ops.set_option("x3_tile", 4)  # (conv_x3h_kernel + fused GroupNorm) wherever its shape allows
+        try:
+            r = paritycheck.pc_vs_golden(dev, net)
+        finally:
+            ops.set_option("x3_tile", 0)
         parity = {k: r[k] for k in ("check", "dtype", "rel_rms", "abs_rms", "golden_rms", "tol_rel", "ok")}
         parity["golden"] = "tests/golden/pc_ouve.npz"
         if r["dtype"] in ("fp32", "fp32x3"):  # the north star's bound: 1e-4 absolute RMS on the complex spectrogram

@@ -776,17 +776,21 @@ constexpr size_t LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
 // s_waitcnt vmcnt(n) for the counts the x3h schedule produces (anything else waits for all)
 SNRSE_DEV void x3h_vm_wait(int n) {
   switch (n) {
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+#define SNRSE_X3H_VM(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    SNRSE_X3H_VM(2) SNRSE_X3H_VM(7) SNRSE_X3H_VM(9) SNRSE_X3H_VM(11) SNRSE_X3H_VM(14) SNRSE_X3H_VM(16)
+    SNRSE_X3H_VM(18) SNRSE_X3H_VM(20)
+#undef SNRSE_X3H_VM
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
 
+// GNM: GroupNorm prologue of the main input as in the bf16 halo kernel (0 none, 1 affine, 2 affine +
+// SiLU), applied once per halo element while it is split: the fp32 mode's gn_act pass disappears.
+template <int GNM>
 __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
   using namespace x3h;
+  constexpr int HOPS = HJ + (GNM > 0 ? 2 : 0);  // vector-memory ops of one halo prefetch per thread
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const ring = smem + 2 * HBYTES;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -824,6 +828,7 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
     hpix[j] = (bb * p.H + ih) * p.W + iw;
   }
   u32x4 hv[HJ];
+  f32x4 gsc, gsh;  // GroupNorm scale / shift of this thread's 4 channels of the prefetched chunk
   auto halo_load = [&](int c) {
     const void* base;
     long long bytes;
@@ -843,21 +848,37 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
       const int voff = hok[j] ? (hpix[j] * cs + cc + hch * 4) * 4 : (int)0x80000000;  // outside: zero padding
       hv[j] = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
     }
+    if constexpr (GNM > 0) {  // issued for shortcut chunks too (unused there): a fixed count per prefetch
+      const long long gb = (long long)p.B * Cin * 4;
+      const int go = ((bb * Cin + (c < cbm ? c : 0) * 32 + hch * 4) * 4);
+      gsc = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(make_rsrc(p.gn_scale, gb), go, 0, 0));
+      gsh = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(make_rsrc(p.gn_shift, gb), go, 0, 0));
+    }
   };
   typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
-  auto halo_store = [&](int buf) {
-    char* const hb = smem + buf * HBYTES;
+  auto halo_store = [&](int c) {  // chunk c's prefetched halo -> halo buffer c & 1
+    char* const hb = smem + (c & 1) * HBYTES;
+    const bool tr = GNM > 0 && c < cbm;
 #pragma unroll
     for (int j = 0; j < HJ; ++j) {
       const int hr = (tid + 512 * j) >> 3;
       if (j == HJ - 1 && hr >= HROWS) break;
-      const u32x4 v = hv[j];
-      const uint32_t h01 = pack_bf16x2(__uint_as_float(v[0]), __uint_as_float(v[1]));
-      const uint32_t h23 = pack_bf16x2(__uint_as_float(v[2]), __uint_as_float(v[3]));
-      const uint32_t l01 = pack_bf16x2(__uint_as_float(v[0]) - __uint_as_float(h01 << 16),
-                                       __uint_as_float(v[1]) - __uint_as_float(h01 & 0xffff0000u));
-      const uint32_t l23 = pack_bf16x2(__uint_as_float(v[2]) - __uint_as_float(h23 << 16),
-                                       __uint_as_float(v[3]) - __uint_as_float(h23 & 0xffff0000u));
+      float x[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x[k] = __uint_as_float(hv[j][k]);
+      if constexpr (GNM > 0) {
+        if (tr) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float y = fmaf(x[k], gsc[k], gsh[k]);
+            x[k] = hok[j] ? (GNM == 2 ? silu(y) : y) : 0.f;  // outside the image: the conv's zero padding
+          }
+        }
+      }
+      const uint32_t h01 = pack_bf16x2(x[0], x[1]);
+      const uint32_t h23 = pack_bf16x2(x[2], x[3]);
+      const uint32_t l01 = pack_bf16x2(x[0] - __uint_as_float(h01 << 16), x[1] - __uint_as_float(h01 & 0xffff0000u));
+      const uint32_t l23 = pack_bf16x2(x[2] - __uint_as_float(h23 << 16), x[3] - __uint_as_float(h23 & 0xffff0000u));
       *(u32x2*)(hb + swz(hr, hch >> 1) + (hch & 1) * 8) = u32x2{h01, h23};
       *(u32x2*)(hb + swz(hr, 4 + (hch >> 1)) + (hch & 1) * 8) = u32x2{l01, l23};
     }
@@ -904,7 +925,7 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
   for (int q = 0; q < nq; ++q) {
     const int c = phase_chunk(q), tp = phase_tap(q);
     // DMA(q) done: wait for all but the ops issued after it (see the schedule in the header comment)
-    x3h_vm_wait(7 * (int)first_with_next(q - 2) + 2 * (int)(q + 1 < nq) + 7 * (int)first_with_next(q - 1));
+    x3h_vm_wait(HOPS * (int)first_with_next(q - 2) + 2 * (int)(q + 1 < nq) + HOPS * (int)first_with_next(q - 1));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (q + 2 < nq) wload(q + 2);
@@ -940,7 +961,7 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
     const bool store_now = c + 1 < ncb && (c < cbm ? tp == 1 : true);
     if (store_now) {
       x3h_vm_wait(q == q0 ? 0 : 2 * (int)(q0 + 3 < nq));
-      halo_store((c + 1) & 1);
+      halo_store(c + 1);
     }
     (void)last_of_chunk;
   }
@@ -1606,14 +1627,21 @@ int launch_x3(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   return (int)hipGetLastError();
 }
 
-int launch_x3h(ConvParams p, hipStream_t s, int tiles) {
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_x3h_kernel,
+template <int GNM>
+int launch_x3h_gn(ConvParams p, hipStream_t s, int tiles) {
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_x3h_kernel<GNM>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)x3h::LDS);
   SNRSE_RET(attr);
   p.ntn = p.Cout / 128;
   p.ksplit = 1;
-  hipLaunchKernelGGL(conv_x3h_kernel, dim3(tiles), dim3(512), x3h::LDS, s, p);
+  hipLaunchKernelGGL(conv_x3h_kernel<GNM>, dim3(tiles), dim3(512), x3h::LDS, s, p);
   return (int)hipGetLastError();
+}
+
+int launch_x3h(const ConvParams& p, hipStream_t s, int tiles) {
+  if (!p.gn_scale) return launch_x3h_gn<0>(p, s, tiles);
+  if (!p.gn_act) return launch_x3h_gn<1>(p, s, tiles);
+  return launch_x3h_gn<2>(p, s, tiles);
 }
 
 template <int BM, int BN, typename TO>
@@ -1696,7 +1724,7 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
   // SNRSE_F32X3: fp32 activations / output, weights pre-split into bf16 hi / lo rows (conv_x3_kernel)
   const bool x3 = dtype == SNRSE_F32X3;
   if (x3) {
-    if (Cout < 128 || Cout % 128 || gn_scale || out_f32) return SNRSE_EINVAL;
+    if (Cout < 128 || Cout % 128 || out_f32) return SNRSE_EINVAL;
     dtype = SNRSE_F32;
   }
   const int KT = dtype == SNRSE_BF16 ? TrB::KT : TrF::KT;
@@ -1743,6 +1771,7 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
         cx.last_ksplit = 1;
         return launch_x3h(q, stream, x3h_tiles);
       }
+      if (q.gn_scale) return SNRSE_EINVAL;  // the fused GroupNorm exists on the halo form only
       cx.last_kernel = 3;
       if (cx.x3_tile == 2) return launch_x3<256, 128, 4, 2>(q, stream, cx);
       if (cx.x3_tile == 3 && q.Cout % 256 == 0) return launch_x3<128, 256, 2, 4>(q, stream, cx);

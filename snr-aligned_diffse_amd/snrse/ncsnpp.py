@@ -210,7 +210,8 @@ class NCSNppHIP:
         (t0, s0), (t1, s1) = x0, (x1 if x1 is not None else (None, None))
         B, H, W, _ = t0.shape
         xs_raw = None
-        if mode == "none" and ops.halo_ok(t0, 3, m.cout):
+        fused = ops.x3h_ok if self.gemm == "x3" else ops.halo_ok  # GEMMs that take GroupNorm+SiLU in their halo
+        if mode == "none" and fused(t0, 3, m.cout):
             gn0 = ops.gn_scale_shift(s0, e["gn0_g"], e["gn0_b"], H * W, sums1=s1)
             h, hs_ = self._conv(t0, e["w0"], 3, m.cout, src1=t1, gn=gn0, bias=e["b0"], temb=dense,
                                 temb_off=e["temb_off"])
@@ -223,7 +224,7 @@ class NCSNppHIP:
             a0 = ops.gn_apply(t0, t1, s0, e["gn0_g"], e["gn0_b"], act=True, mode=mode, sums1=s1)
             h, hs_ = self._conv(a0, e["w0"], 3, m.cout, bias=e["b0"], temb=dense, temb_off=e["temb_off"])
         Hh, Wh = h.shape[1], h.shape[2]
-        if ops.halo_ok(h, 3, m.cout):
+        if fused(h, 3, m.cout):
             src, gn1 = h, ops.gn_scale_shift(hs_, e["gn1_g"], e["gn1_b"], Hh * Wh)
         else:
             src, gn1 = ops.gn_apply(h, None, hs_, e["gn1_g"], e["gn1_b"], act=True), None

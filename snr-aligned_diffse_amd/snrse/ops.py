@@ -185,7 +185,7 @@ def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_w
     return out
 
 
-_VARIANT = {"v": 0}
+_VARIANT = {"v": 0, "x3_tile": 0}
 
 
 def get_option(name):
@@ -249,6 +249,18 @@ def halo_ok(x, ksize, cout):
     # the split-K GEMM (faster there: profiles/r03v_level4_halo_vs_glds.jsonl)
     return (x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and H % 4 == 0 and W % 64 == 0
             and _VARIANT["v"] in (0, 5))
+
+
+def x3h_ok(x, ksize, cout):
+    """True when a split-bf16 fp32 conv (fp32 x, ops.split_weight weights) takes the halo kernel
+    (conv_x3h_kernel) under the current x3_tile setting -- the one form that accepts a fused GroupNorm
+    (gn=).  Mirrors snrse_conv2d's dispatch: 3x3, H % 4 == 0, W % 64 == 0 and >= 256 tiles of
+    4 x 64 px x 128 couts (x3_tile 0), or wherever legal (x3_tile 4)."""
+    B, H, W, C = x.shape
+    if x.dtype != torch.float32 or ksize != 3 or cout % 128 or H % 4 or W % 64:
+        return False
+    t = _VARIANT["x3_tile"]
+    return t == 4 or (t == 0 and B * (H // 4) * (W // 64) * (cout // 128) >= 256)
 
 
 def head_ok(x):
@@ -603,6 +615,8 @@ def set_option(name: str, value: int):
         c.set_option(name, value)
     if name == "conv_variant":
         _VARIANT["v"] = int(value)
+    if name == "x3_tile":
+        _VARIANT["x3_tile"] = int(value)
 
 
 def spec_transform(spec, direction):

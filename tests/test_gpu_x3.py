@@ -123,6 +123,42 @@ def test_x3_level0_vs_exact_fp32(gpu):
     assert rel(ops.fold_stats(st_b), ops.fold_stats(st_a)) < 1e-5
 
 
+@pytest.mark.parametrize("act", [True, False])
+@pytest.mark.parametrize("shape", [(2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (2, 256, 128, 4, 64)])
+def test_x3h_fused_groupnorm_silu(gpu, shape, act):
+    """The halo form consuming SiLU(GN(x)) (act) or GN(x) from raw fp32 x + per-(b, c) scale / shift, with a
+    raw 1x1 shortcut as extra K; every other split conv rejects a fused GroupNorm."""
+    from snrse import ops
+    B, cin, cout, H, W = shape
+    x = torch.from_numpy(fnormal("t.fg.x", (B, cin, H, W))) * 1.5 + 0.2
+    w = torch.from_numpy(fnormal("t.fg.w", (cout, cin, 3, 3))) / math.sqrt(9 * cin)
+    g = torch.from_numpy(fnormal("t.fg.g", (cin,))) * 0.1 + 1
+    be = torch.from_numpy(fnormal("t.fg.b", (cin,))) * 0.1
+    xs = torch.from_numpy(fnormal("t.fg.xs", (B, 128, H, W)))
+    w2 = torch.from_numpy(fnormal("t.fg.w2", (cout, 128, 1, 1))) / 11
+    a = F.group_norm(x.double(), min(cin // 4, 32), g.double(), be.double(), eps=1e-6)
+    a = F.silu(a) if act else a
+    ref = F.conv2d(a, w.double(), padding=1) + F.conv2d(xs.double(), w2.double())
+    xg = nhwc(x).to(gpu)
+    c0 = 256 if cin == 384 else cin
+    s0, s1 = (xg[..., :c0].contiguous(), xg[..., c0:].contiguous()) if c0 != cin else (xg, None)
+    sums = ops.gn_stats(s0, s1)
+    gn = ops.gn_scale_shift(sums[0], g.to(gpu), be.to(gpu), H * W, sums1=sums[1])
+    wp = ops.split_weight(w.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu))
+    w2p = ops.split_weight(w2.reshape(cout, 128).to(gpu))
+    assert not ops.x3h_ok(s0, 3, cout)  # a small grid: the register-staged form, which has no GroupNorm
+    with pytest.raises(RuntimeError):
+        ops.conv2d(s0, wp, 3, cout, src1=s1, gn=gn, gn_act=act, sc=nhwc(xs).to(gpu), sc_wgt=w2p)
+    ops.set_option("x3_tile", 4)
+    try:
+        assert ops.x3h_ok(s0, 3, cout)
+        out = ops.conv2d(s0, wp, 3, cout, src1=s1, gn=gn, gn_act=act, sc=nhwc(xs).to(gpu), sc_wgt=w2p)
+        assert ops.get_option("last_kernel") == 4
+    finally:
+        ops.set_option("x3_tile", 0)
+    assert rel(nchw(out), ref) < TOL
+
+
 @pytest.fixture(scope="module")
 def net_x3(gpu):
     from snrse import ncsnpp
@@ -130,7 +166,17 @@ def net_x3(gpu):
     return ncsnpp.NCSNppHIP(sd, dtype=torch.float32, device=gpu, gemm="x3")
 
 
-def test_x3_ncsnpp_full_golden(gpu, net_x3):
+@pytest.fixture(params=[0, 4], ids=["auto", "halo_forced"])
+def x3_tile(request):
+    """x3_tile 0: at the goldens' [2, 256, 64] grid every split conv is register-staged (+ gn_act);
+    4: the halo kernel with the fused GroupNorm wherever W % 64 == 0 (the benched form at C2 sizes)."""
+    from snrse import ops
+    ops.set_option("x3_tile", request.param)
+    yield request.param
+    ops.set_option("x3_tile", 0)
+
+
+def test_x3_ncsnpp_full_golden(gpu, net_x3, x3_tile):
     g = golden("ncsnpp_full.npz")
     x = torch.from_numpy(fnormal("golden.ncsnpp.x", (2, 2, 256, 64), complex_=True)) * 0.5
     t = torch.tensor([0.5, 0.8], device=gpu)
@@ -139,7 +185,7 @@ def test_x3_ncsnpp_full_golden(gpu, net_x3):
     assert abs_rms(out, g["out"][:, 0]) < 1e-4
 
 
-def test_x3_pc_loop_vs_reference_golden(gpu, net_x3):
+def test_x3_pc_loop_vs_reference_golden(gpu, net_x3, x3_tile):
     """The benched class (PCEnhancer) in the fp32x3 mode on the reference's N=5 OUVE run."""
     import paritycheck
     r = paritycheck.pc_vs_golden(gpu, net_x3)
