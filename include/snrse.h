@@ -146,8 +146,8 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  * "h5_tw" halo-GEMM tile: 0 auto (8 rows x 32 px where H % 8 == 0, else 4 x 64), 64 forces 4 x 64;
  * "resample_variant" 0 row-strip / 1 LDS-tiled gn_resample, "resample_nt" non-temporal stores there,
  * "resample_down_rows" 1 / 2 / 4 (default) output rows per down-sampling row strip (bit-identical results);
- * "x3_tile" split-bf16 fp32 GEMM: 0 auto (the halo kernel on 3x3 convs with H % 4 == 0, W % 64 == 0 and >= 256
- *   tiles of 4 x 64 px x 128 couts, else register-staged 128 x 128), register-staged tiles 1 128 px x 128 couts,
+ * "x3_tile" split-bf16 fp32 GEMM: 0 auto (the halo kernel on 3x3 convs with H % 4 == 0 and >= 256 tiles of
+ *   4 x 64 px x 128 couts, any W, else register-staged 128 x 128), register-staged tiles 1 128 px x 128 couts,
  *   2 256 x 128, 3 128 x 256 (Cout % 256 == 0), 4 the halo kernel wherever its shape conditions hold;
  * "stats_zeroed" 1 = the statistics buffers handed to snrse_conv2d / snrse_gn_stats are already zero (the
  * caller clears one arena per network evaluation), so they skip their per-call memset. */

@@ -49,6 +49,7 @@ int* option_field(snrse_ctx& c, const char* name) {
   if (name_is(name, "resample_nt")) return &c.resample_nt;
   if (name_is(name, "resample_down_rows")) return &c.resample_down_rows;
   if (name_is(name, "x3_tile")) return &c.x3_tile;
+  if (name_is(name, "x3_spread")) return &c.x3_spread;
   return nullptr;
 }
 

@@ -100,7 +100,8 @@ struct snrse_ctx {
   int resample_variant = 0;    // 0 row-strip, 1 LDS-tiled gn_resample
   int resample_nt = 0;         // non-temporal stores in gn_resample
   int resample_down_rows = 4;  // output rows per down-sampling row strip (1, 2, 4; 4 fastest since r03)
-  int x3_tile = 0;             // split-bf16 fp32 GEMM tile: 0 auto, 1 128x128, 2 256x128, 3 128x256
+  int x3_tile = 0;             // split-bf16 fp32 GEMM tile: 0 auto, 1 128x128, 2 256x128, 3 128x256, 4 halo
+  int x3_spread = 1;           // halo split GEMM: next chunk's halo stored one piece per tap (0: in one go)
   // split-K workspace: [splits][M][Cout] f32 partial sums (NULL: no splitting)
   float* ws = nullptr;
   size_t ws_bytes = 0;

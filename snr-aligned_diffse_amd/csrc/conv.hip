@@ -56,9 +56,11 @@ SNRSE_DEV void block_stats_flush(const ConvParams& p, const float* red, int blk_
   }
 }
 
+// nvalid < 64: only the wave's first nvalid rows are output pixels (a tile cut by the image's right
+// edge, conv_x3h_kernel); the rest are skipped.
 template <typename TO, int NWM, int BN, bool DEFER = false>
 SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int mb, int nb, int lane, float* stage,
-                            float* red, int wm, int blk_b, int blk_n0) {
+                            float* red, int wm, int blk_b, int blk_n0, int nvalid = 64) {
   constexpr int LDR = 68;  // padded row (floats): conflict-free C-layout writes
   constexpr int EPC = 16 / (int)sizeof(TO);  // outputs per 16-B chunk (8 bf16 / 4 f32)
   constexpr int NCH = 64 / EPC;              // chunks per row
@@ -88,7 +90,7 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
       cb[k] = p.comb_b[n + k];
     }
   }
-  const int m_last = min(mb + 63, p.M - 1);
+  const int m_last = min(mb + nvalid - 1, p.M - 1);
   const bool one_b = mb < p.M && (mb / HW) == (m_last / HW);
   float s1[EPC], s2[EPC];
 #pragma unroll
@@ -97,7 +99,7 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
   for (int pass = 0; pass < 64 / RPP; ++pass) {
     const int row = r0 + pass * RPP;
     const int m = mb + row;
-    if (m >= p.M || !nok) continue;
+    if (m >= p.M || !nok || row >= nvalid) continue;
     float v[EPC];
     const float* sr = stage + row * LDR + cc * EPC;
 #pragma unroll
@@ -787,7 +789,7 @@ SNRSE_DEV void x3h_vm_wait(int n) {
 
 // GNM: GroupNorm prologue of the main input as in the bf16 halo kernel (0 none, 1 affine, 2 affine +
 // SiLU), applied once per halo element while it is split: the fp32 mode's gn_act pass disappears.
-template <int GNM>
+template <int GNM, bool SPR>
 __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
   using namespace x3h;
   constexpr int HOPS = HJ + (GNM > 0 ? 2 : 0);  // vector-memory ops of one halo prefetch per thread
@@ -801,7 +803,7 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
   const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
   const int n0 = (g % p.ntn) * 128;
   int tile = g / p.ntn;
-  const int ntw = p.W / TW, nth = p.H / TH;
+  const int ntw = (p.W + TW - 1) / TW, nth = p.H / TH;  // the last tile column may be cut by the image edge
   const int w0 = (tile % ntw) * TW;
   tile /= ntw;
   const int h0 = (tile % nth) * TH;
@@ -815,7 +817,8 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
   const int nq = 9 * cbm + cbs;
   const int K1 = 9 * Cin;
 
-  // this thread's halo pieces: halo row (tid + 512 j) >> 3, 16-B fp32 chunk tid & 7 (4 channels)
+  // this thread's halo pieces: halo row (tid + 512 j) >> 3, 16-B fp32 chunk tid & 7 (4 channels); pixels
+  // outside the image (the padding ring, and the columns past a cut tile's edge) load as zero
   const int hch = tid & 7;
   int hpix[HJ];
   bool hok[HJ];
@@ -883,6 +886,32 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
       *(u32x2*)(hb + swz(hr, 4 + (hch >> 1)) + (hch & 1) * 8) = u32x2{l01, l23};
     }
   };
+  // SPR: one halo piece j (this thread's 16-B fp32 vector of halo row (tid + 512 j) >> 3) of the prefetched
+  // chunk, split (+ GroupNorm) and stored branch-free -- placed after a tap's MFMAs so the scheduler can
+  // interleave its VALU with them; tr = the chunk is a main-input chunk (GroupNorm applies)
+  auto halo_piece = [&](char* hb, int j, bool tr) {
+    const int hr = (tid + 512 * j) >> 3;
+    float x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = __uint_as_float(hv[j][k]);
+    if constexpr (GNM > 0) {
+      const uint32_t keep = tr ? 0u : ~0u, zero = (hok[j] || !tr) ? ~0u : 0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float y = fmaf(x[k], gsc[k], gsh[k]);
+        const float z = GNM == 2 ? silu(y) : y;
+        x[k] = __uint_as_float(((__float_as_uint(z) & ~keep) | (__float_as_uint(x[k]) & keep)) & zero);
+      }
+    }
+    const uint32_t h01 = pack_bf16x2(x[0], x[1]);
+    const uint32_t h23 = pack_bf16x2(x[2], x[3]);
+    const uint32_t l01 = pack_bf16x2(x[0] - __uint_as_float(h01 << 16), x[1] - __uint_as_float(h01 & 0xffff0000u));
+    const uint32_t l23 = pack_bf16x2(x[2] - __uint_as_float(h23 << 16), x[3] - __uint_as_float(h23 & 0xffff0000u));
+    if (j < HJ - 1 || hr < HROWS) {
+      *(u32x2*)(hb + swz(hr, hch >> 1) + (hch & 1) * 8) = u32x2{h01, h23};
+      *(u32x2*)(hb + swz(hr, 4 + (hch >> 1)) + (hch & 1) * 8) = u32x2{l01, l23};
+    }
+  };
   // phase q -> (chunk, tap): main chunks 9 taps each, then the shortcut chunks' center tap
   auto phase_chunk = [&](int q) { return q < 9 * cbm ? q / 9 : cbm + (q - 9 * cbm); };
   auto phase_tap = [&](int q) { return q < 9 * cbm ? q - (q / 9) * 9 : 4; };
@@ -892,19 +921,21 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
     return (c < cbm ? phase_tap(q) == 0 : true) && c + 1 < ncb;
   };
   // weights of phase q -> ring slot q % 3: 16 pieces of 1 KB (8 rows x 128 B), 2 per wave
-  auto wload = [&](int q) {
+  auto wload = [&](int q) {  // q >= nq (SPR's branch-free schedule): zero-filling out-of-range loads
+    const bool oob = q >= nq;
+    char* dst = ring + (q % 3) * TAPB;  // slot q % 3 even when out of range: never read again
+    if (oob) q = nq - 1;
     const int c = phase_chunk(q), tp = phase_tap(q);
     const bool mainw = c < cbm;
     const int wld = mainw ? 2 * K1 : 2 * Csc_all;                      // bf16 elements per row
     const int koff = mainw ? 2 * (tp * Cin + c * 32) : 2 * ((c - cbm) * 32);
     const __amdgpu_buffer_rsrc_t r = mainw ? make_rsrc(p.wgt, p.wbytes) : make_rsrc(p.sc_wgt, p.sc_wbytes);
-    char* dst = ring + (q % 3) * TAPB;
     const int rl = lane >> 3, sl = lane & 7;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int pc = wid * 2 + k;
       const int row = pc * 8 + rl;
-      const unsigned voff = (unsigned)(((n0 + row) * wld + koff + (sl ^ (row & 7)) * 8) * 2);
+      const unsigned voff = oob ? 0x80000000u : (unsigned)(((n0 + row) * wld + koff + (sl ^ (row & 7)) * 8) * 2);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(dst + pc * 1024), 16,
                                                voff, 0, 0, 0);
     }
@@ -922,6 +953,70 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   halo_store(0);
   const int lrow = lane & 15, lg = lane >> 4;
+  // one tap's fragment reads + 48 MFMAs from halo buffer hb and ring slot sb
+  auto tap_mfma = [&](const char* hb, const char* sb, int tp) {
+    const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
+    const int hbase = (wr + dy + 1) * HC + dx + 1 + lrow;
+    u32x4 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ah[i] = *(const u32x4*)(hb + swz(hbase + 16 * i, lg));
+      al[i] = *(const u32x4*)(hb + swz(hbase + 16 * i, 4 + lg));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bh[j] = *(const u32x4*)(sb + swz(wc * 64 + j * 16 + lrow, lg));
+      bl[j] = *(const u32x4*)(sb + swz(wc * 64 + j * 16 + lrow, 4 + lg));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j] = mfma_chunk<bf16_t>(ah[i], bh[j], acc[i][j]);
+        acc[i][j] = mfma_chunk<bf16_t>(ah[i], bl[j], acc[i][j]);
+        acc[i][j] = mfma_chunk<bf16_t>(al[i], bh[j], acc[i][j]);
+      }
+  };
+  if constexpr (SPR) {
+    // Branch-free schedule: every phase issues its DMA two phases ahead (zero-filling past the end), every
+    // chunk prefetches the next one's halo at its first phase (the last chunk re-reads itself into the
+    // unused buffer), so the ops issued after DMA(q) are DMA(q+1) plus the halo prefetches of phases q-1 /
+    // q-2 when those start a chunk.  Main chunks: the prefetched halo is stored one piece per tap, after
+    // the MFMAs of taps 2..8 (the wait at the top of tap 2 covers the halo loads).
+    int q = 0;
+    for (int c = 0; c < cbm; ++c) {
+      const bool tr = c + 1 < cbm;
+      char* const nb_ = smem + ((c + 1) & 1) * HBYTES;
+      const char* const hb = smem + (c & 1) * HBYTES;
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp, ++q) {
+        // DMA(q): ops issued after it are DMA(q+1) and, at tap 1, this chunk's halo prefetch; at tap 2 the
+        // prefetch is waited for too (its pieces are stored from this tap on)
+        if (tp == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + HOPS) : "memory");
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        wload(q + 2);
+        if (tp == 0) halo_load(c + 1 < ncb ? c + 1 : c);
+        tap_mfma(hb, ring + (q % 3) * TAPB, tp);
+        if (tp >= 2) halo_piece(nb_, tp - 2, tr);
+      }
+    }
+    for (int c = cbm; c < ncb; ++c, ++q) {
+      const int qa = q - 2, qb = q - 1;  // phase-first flags of the two previous phases
+      const bool fa = qa >= 0 && (qa >= 9 * cbm || qa % 9 == 0), fb = qb >= 0 && (qb >= 9 * cbm || qb % 9 == 0);
+      x3h_vm_wait(2 + HOPS * (int)fa + HOPS * (int)fb);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      wload(q + 2);
+      halo_load(c + 1 < ncb ? c + 1 : c);
+      tap_mfma(smem + (c & 1) * HBYTES, ring + (q % 3) * TAPB, 4);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      char* const nb_ = smem + ((c + 1) & 1) * HBYTES;
+#pragma unroll
+      for (int j = 0; j < HJ; ++j) halo_piece(nb_, j, false);
+    }
+  } else
   for (int q = 0; q < nq; ++q) {
     const int c = phase_chunk(q), tp = phase_tap(q);
     // DMA(q) done: wait for all but the ops issued after it (see the schedule in the header comment)
@@ -969,7 +1064,7 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
   __builtin_amdgcn_s_barrier();  // LDS is reused as the epilogue staging area
   const int mb = (bb * p.H + h0 + wr) * p.W + w0;
   epilogue_lds<float, 4, 128>(p, acc, mb, n0 + wc * 64, lane, (float*)(smem + wid * (64 * 68 * 4)),
-                              (float*)(smem + 8 * (64 * 68 * 4)), wr, bb, n0);
+                              (float*)(smem + 8 * (64 * 68 * 4)), wr, bb, n0, min(TW, p.W - w0));
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1627,21 +1722,26 @@ int launch_x3(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   return (int)hipGetLastError();
 }
 
-template <int GNM>
+template <int GNM, bool SPR>
 int launch_x3h_gn(ConvParams p, hipStream_t s, int tiles) {
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_x3h_kernel<GNM>,
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_x3h_kernel<GNM, SPR>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)x3h::LDS);
   SNRSE_RET(attr);
   p.ntn = p.Cout / 128;
   p.ksplit = 1;
-  hipLaunchKernelGGL(conv_x3h_kernel<GNM>, dim3(tiles), dim3(512), x3h::LDS, s, p);
+  hipLaunchKernelGGL((conv_x3h_kernel<GNM, SPR>), dim3(tiles), dim3(512), x3h::LDS, s, p);
   return (int)hipGetLastError();
 }
 
-int launch_x3h(const ConvParams& p, hipStream_t s, int tiles) {
-  if (!p.gn_scale) return launch_x3h_gn<0>(p, s, tiles);
-  if (!p.gn_act) return launch_x3h_gn<1>(p, s, tiles);
-  return launch_x3h_gn<2>(p, s, tiles);
+template <bool SPR>
+int launch_x3h_spr(const ConvParams& p, hipStream_t s, int tiles) {
+  if (!p.gn_scale) return launch_x3h_gn<0, SPR>(p, s, tiles);
+  if (!p.gn_act) return launch_x3h_gn<1, SPR>(p, s, tiles);
+  return launch_x3h_gn<2, SPR>(p, s, tiles);
+}
+
+int launch_x3h(const ConvParams& p, hipStream_t s, int tiles, int spread) {
+  return spread ? launch_x3h_spr<true>(p, s, tiles) : launch_x3h_spr<false>(p, s, tiles);
 }
 
 template <int BM, int BN, typename TO>
@@ -1764,12 +1864,12 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
   if (dtype != SNRSE_BF16 && dtype != SNRSE_F32) return SNRSE_EINVAL;
   auto run = [&](const ConvParams& q) {
     if (x3) {
-      const int x3h_tiles = q.B * (q.H / x3h::TH) * (q.W / x3h::TW) * (q.Cout / 128);
-      const bool x3h_ok = q.ksize == 3 && q.H % x3h::TH == 0 && q.W % x3h::TW == 0;
+      const int x3h_tiles = q.B * (q.H / x3h::TH) * ((q.W + x3h::TW - 1) / x3h::TW) * (q.Cout / 128);
+      const bool x3h_ok = q.ksize == 3 && q.H % x3h::TH == 0;
       if (x3h_ok && ((cx.x3_tile == 0 && x3h_tiles >= 256) || cx.x3_tile == 4)) {
         cx.last_kernel = 4;
         cx.last_ksplit = 1;
-        return launch_x3h(q, stream, x3h_tiles);
+        return launch_x3h(q, stream, x3h_tiles, cx.x3_spread);
       }
       if (q.gn_scale) return SNRSE_EINVAL;  // the fused GroupNorm exists on the halo form only
       cx.last_kernel = 3;

@@ -254,13 +254,13 @@ def halo_ok(x, ksize, cout):
 def x3h_ok(x, ksize, cout):
     """True when a split-bf16 fp32 conv (fp32 x, ops.split_weight weights) takes the halo kernel
     (conv_x3h_kernel) under the current x3_tile setting -- the one form that accepts a fused GroupNorm
-    (gn=).  Mirrors snrse_conv2d's dispatch: 3x3, H % 4 == 0, W % 64 == 0 and >= 256 tiles of
-    4 x 64 px x 128 couts (x3_tile 0), or wherever legal (x3_tile 4)."""
+    (gn=).  Mirrors snrse_conv2d's dispatch: 3x3, H % 4 == 0 and >= 256 tiles of 4 x 64 px x 128 couts
+    (the last tile column cut by the image edge; x3_tile 0), or wherever legal (x3_tile 4)."""
     B, H, W, C = x.shape
-    if x.dtype != torch.float32 or ksize != 3 or cout % 128 or H % 4 or W % 64:
+    if x.dtype != torch.float32 or ksize != 3 or cout % 128 or H % 4:
         return False
     t = _VARIANT["x3_tile"]
-    return t == 4 or (t == 0 and B * (H // 4) * (W // 64) * (cout // 128) >= 256)
+    return t == 4 or (t == 0 and B * (H // 4) * (-(-W // 64)) * (cout // 128) >= 256)
 
 
 def head_ok(x):

@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tiles", default="0,1,3")
     ap.add_argument("--exact", type=int, default=1)
+    ap.add_argument("--gn", type=int, default=0, help="1: fused GroupNorm+SiLU on the x3h variants (x3_tile 0)")
+    ap.add_argument("--spread", default="1", help="x3_spread settings to run each split variant with")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
@@ -49,12 +51,21 @@ def main():
         out = torch.empty(B, H, W, Co, device=dev)
         st = ops.new_stats(B, Co)
         flops = 2.0 * B * H * W * Co * 9 * (C0 + C1)
-        variants = [("x3", t) for t in map(int, args.tiles.split(","))] + ([("exact", 0)] if args.exact else [])
+        spreads = list(map(int, args.spread.split(",")))
+        variants = [("x3", t, sp) for t in map(int, args.tiles.split(",")) for sp in spreads]
+        variants += [("exact", 0, 0)] if args.exact else []
+        gn = None
+        if args.gn:
+            sc = torch.rand(B, C0 + C1, device=dev, generator=g) + 0.5
+            gn = (sc, torch.randn(B, C0 + C1, device=dev, generator=g) * 0.1)
+            variants = [("x3gn", 0, sp) for sp in spreads] + variants
         ref = None
-        for kind, t in variants:
+        for kind, t, sp in variants:
             ops.set_option("x3_tile", t)
-            wt = ws if kind == "x3" else w
-            fn = lambda: ops.conv2d(x0, wt, 3, Co, bias=b, src1=x1, out=out, stats=st)  # noqa: E731
+            ops.set_option("x3_spread", sp)
+            wt = w if kind == "exact" else ws
+            kw = {"gn": gn} if kind == "x3gn" else {}
+            fn = lambda: ops.conv2d(x0, wt, 3, Co, bias=b, src1=x1, out=out, stats=st, **kw)  # noqa: E731
             ms = time_call(fn, args.reps)
             fn()
             torch.cuda.synchronize()
@@ -62,10 +73,11 @@ def main():
             if ref is None:
                 ref = o
             err = float((o - ref).pow(2).mean().sqrt() / ref.pow(2).mean().sqrt())
-            print(json.dumps({"shape": [B, C0, C1, Co, H, W], "kind": kind, "tile": t, "ms": ms,
+            print(json.dumps({"shape": [B, C0, C1, Co, H, W], "kind": kind, "tile": t, "spread": sp, "ms": ms,
                               "tflops": flops / ms / 1e9, "kernel": ops.kernel_name(ops.get_option("last_kernel")),
                               "ksplit": ops.get_option("last_ksplit"), "rel_vs_first": err}), flush=True)
         ops.set_option("x3_tile", 0)
+        ops.set_option("x3_spread", 1)
         del x0, x1, out, ref
 
 
