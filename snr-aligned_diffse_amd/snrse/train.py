@@ -100,6 +100,26 @@ def _pack(w, cin_pad, rows):
     return p.contiguous()
 
 
+# GEMM arithmetic of the training convs (forward and input-gradient): "exact" fp32 MFMA, or "x3" -- the
+# split-bf16 fp32 GEMM of the fp32x3 mode (ops.split_weight; ~2^-16 relative per product), for every conv
+# whose weight matrix has >= 128 rows (the Cout <= 16 pyramid heads and their likes stay exact).  The
+# weight gradient (snrse_conv_wgrad) is exact fp32 either way.
+_GEMM = {"mode": "exact"}
+
+
+def set_gemm(mode):
+    if mode not in ("exact", "x3"):
+        raise ValueError(f"snrse.train: gemm mode {mode!r}")
+    _GEMM["mode"] = mode
+
+
+def _wmat(wp):
+    rows, k = wp.shape
+    if _GEMM["mode"] == "x3" and rows % 128 == 0 and k % 32 == 0:
+        return ops.split_weight(wp)
+    return wp
+
+
 def _rows(cout):
     if cout >= 64:
         if cout % 128:
@@ -122,7 +142,7 @@ class _Conv(torch.autograd.Function):
         if x1 is not None and (C0 % 32 or x1.shape[-1] % 32):
             raise ValueError("concatenated conv inputs need 32-channel multiples")
         x0p = x0 if x1 is not None else _pad_last(x0.contiguous(), _ceil(C0, 32))
-        wp = _pack(w, x0p.shape[-1] + (0 if x1 is None else x1.shape[-1]), _rows(cout))
+        wp = _wmat(_pack(w, x0p.shape[-1] + (0 if x1 is None else x1.shape[-1]), _rows(cout)))
         out = ops.conv2d(x0p.contiguous(), wp, k, cout, bias=None if b is None else b.detach().contiguous(),
                          src1=None if x1 is None else x1.contiguous(),
                          res=None if res is None else res.detach().contiguous(), out_scale=scale,
@@ -158,7 +178,7 @@ class _Conv(torch.autograd.Function):
             wt = w.detach().flip(2, 3).permute(1, 0, 2, 3)  # [Cin, Cout, k, k]
             cp = _ceil(cout, 32)
             dpad = _pad_last(d, cp)
-            wtp = _pack(wt.contiguous(), cp, _rows(cin))
+            wtp = _wmat(_pack(wt.contiguous(), cp, _rows(cin)))
             dx = ops.conv2d(dpad.contiguous(), wtp, k, cin)
             if x1 is None:
                 dx0 = dx
