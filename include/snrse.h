@@ -87,7 +87,8 @@ int snrse_upfirdn2d(const void* in, void* out, const float* kernel, int major, i
  *          hipErrorInvalidValue).
  *   dtype SNRSE_F32X3: src/res/out fp32; wgt [Npad][2*ksize*ksize*(C0+C1)] and sc_wgt [Npad][2*(Csc+Csc1)]
  *          bf16, each 32-element K-tile of the fp32 packing stored as 32 hi = bf16(w) then 32
- *          lo = bf16(w - hi); Cout % 128 == 0, no gn_scale / out_f32 (else hipErrorInvalidValue). */
+ *          lo = bf16(w - hi); Cout % 128 == 0 or Cout <= 16 (Npad 16); gn_scale only on the halo form
+ *          (3x3, H % 4 == 0, >= 256 tiles or option x3_tile 4), else hipErrorInvalidValue; out_f32 ignored. */
 int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void* src1, int C1, int B, int H, int W, int ksize,
                  const void* wgt, const void* sc_src, int Csc, const void* sc_src1, int Csc1,
                  const void* sc_wgt, const float* bias, const float* temb, int temb_stride,

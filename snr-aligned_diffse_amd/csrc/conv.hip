@@ -1706,10 +1706,10 @@ int launch_x3(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   static const hipError_t attr = hipFuncSetAttribute((const void*)conv_x3_kernel<BM, BN, WM, WN>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   SNRSE_RET(attr);
-  p.ntn = p.Cout / BN;
+  p.ntn = (p.Cout + BN - 1) / BN;
   const int tiles = ((p.M + BM - 1) / BM) * p.ntn;
   const int nk = p.ksize * p.ksize * ((p.C0 + p.C1) / 32) + (p.sc_src ? (p.Csc + p.Csc1) / 32 : 0);
-  p.ksplit = choose_ksplit(p, tiles, nk, cx, 2);
+  p.ksplit = BN == 128 ? choose_ksplit(p, tiles, nk, cx, 2) : 1;  // (the finalize works on 128-cout rows)
   p.ws = cx.ws;
   cx.last_ksplit = p.ksplit;
   hipLaunchKernelGGL((conv_x3_kernel<BM, BN, WM, WN>), dim3(tiles * p.ksplit), dim3(64 * WM * WN), lds, s, p);
@@ -1824,8 +1824,9 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
   // SNRSE_F32X3: fp32 activations / output, weights pre-split into bf16 hi / lo rows (conv_x3_kernel)
   const bool x3 = dtype == SNRSE_F32X3;
   if (x3) {
-    if (Cout < 128 || Cout % 128 || out_f32) return SNRSE_EINVAL;
+    if (Cout > 16 && Cout % 128) return SNRSE_EINVAL;  // 128-cout tiles, or one 16-row tile (pyramid heads)
     dtype = SNRSE_F32;
+    out_f32 = 0;  // (the output is fp32 anyway)
   }
   const int KT = dtype == SNRSE_BF16 ? TrB::KT : TrF::KT;
   if (!src0 || !wgt || !out || (ksize != 1 && ksize != 3)) return SNRSE_EINVAL;
@@ -1865,7 +1866,7 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
   auto run = [&](const ConvParams& q) {
     if (x3) {
       const int x3h_tiles = q.B * (q.H / x3h::TH) * ((q.W + x3h::TW - 1) / x3h::TW) * (q.Cout / 128);
-      const bool x3h_ok = q.ksize == 3 && q.H % x3h::TH == 0;
+      const bool x3h_ok = q.ksize == 3 && q.H % x3h::TH == 0 && q.Cout % 128 == 0;
       if (x3h_ok && ((cx.x3_tile == 0 && x3h_tiles >= 256) || cx.x3_tile == 4)) {
         cx.last_kernel = 4;
         cx.last_ksplit = 1;
@@ -1873,6 +1874,7 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
       }
       if (q.gn_scale) return SNRSE_EINVAL;  // the fused GroupNorm exists on the halo form only
       cx.last_kernel = 3;
+      if (q.Cout <= 16) return launch_x3<128, 16, 4, 1>(q, stream, cx);  // the pyramid heads (16 padded rows)
       if (cx.x3_tile == 2) return launch_x3<256, 128, 4, 2>(q, stream, cx);
       if (cx.x3_tile == 3 && q.Cout % 256 == 0) return launch_x3<128, 256, 2, 4>(q, stream, cx);
       return launch_x3<128, 128, 2, 2>(q, stream, cx);

@@ -101,8 +101,24 @@ def test_x3_residual_and_layout_errors(gpu):
     assert rel(nchw(out), ref) < TOL
     with pytest.raises(TypeError):  # split main weights with exact shortcut weights
         ops.conv2d(nhwc(x).to(gpu), ops.split_weight(wp), 1, C, sc=nhwc(x).to(gpu), sc_wgt=wp)
-    with pytest.raises(RuntimeError):  # Cout < 128 has no split kernel (the pyramid heads stay exact fp32)
-        ops.conv2d(nhwc(x).to(gpu), ops.split_weight(torch.zeros(16, 9 * C, device=gpu)), 3, 4)
+    with pytest.raises(RuntimeError):  # 16 < Cout, Cout % 128 != 0: no split tile
+        ops.conv2d(nhwc(x).to(gpu), ops.split_weight(torch.zeros(64, 9 * C, device=gpu)), 3, 64)
+
+
+def test_x3_pyramid_head(gpu):
+    """Cout = 4 (16 padded rows) with the upsampled pyramid as an fp32 residual: the heads' split GEMM."""
+    from snrse import ops
+    B, cin, H, W = 2, 256, 8, 16
+    x = torch.from_numpy(fnormal("t.py.x", (B, cin, H, W)))
+    w = torch.from_numpy(fnormal("t.py.w", (4, cin, 3, 3))) / 48
+    b = torch.from_numpy(fnormal("t.py.b", (4,)))
+    r = torch.from_numpy(fnormal("t.py.r", (B, 4, H, W)))
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1) + r.double()
+    wp = torch.cat([w.permute(0, 2, 3, 1).reshape(4, -1), torch.zeros(12, 9 * cin)]).to(gpu)
+    out = ops.conv2d(nhwc(x).to(gpu), ops.split_weight(wp), 3, 4, bias=b.to(gpu), res=nhwc(r).to(gpu), out_f32=True)
+    assert ops.get_option("last_kernel") == 3
+    assert out.dtype == torch.float32
+    assert rel(nchw(out), ref) < TOL
 
 
 def test_x3_level0_vs_exact_fp32(gpu):
