@@ -249,6 +249,10 @@ size_t snrse_snrnet_workspace(int B, int T);
  * X is the channel concatenation of x0 [.., C0] and x1 [.., C1]; dw must be zeroed by the caller. */
 int snrse_conv_wgrad(const float* dy, int Cout, const float* x0, int C0, const float* x1, int C1, int B, int H,
                      int W, int ksize, float* dw, hipStream_t stream);
+/* The same with split-bf16 products (fp32 in and out; dY and X split into bf16 hi / lo, three bf16 MFMA
+ * products per block): the fp32x3 training mode.  Cout, C0, C1 multiples of 4. */
+int snrse_conv_wgrad_x3(const float* dy, int Cout, const float* x0, int C0, const float* x1, int C1, int B, int H,
+                        int W, int ksize, float* dw, hipStream_t stream);
 /* scale * per-(b, c) sums over the HW pixels of x [B][HW][C] added into out_bc [B][C] and / or the
  * per-c total into out_c [C] (bias, Dense_0 and temb gradients). */
 int snrse_chan_sum(const float* x, int B, int HW, int C, float* out_bc, float* out_c, float scale,

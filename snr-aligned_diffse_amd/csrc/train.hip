@@ -3,6 +3,7 @@
 // torch.optim.Adam + torch_ema, model.py:99-106).  fp32 throughout, NHWC activations.
 //
 //   snrse_conv_wgrad      dW[co][tap][ci] += sum_p dY[p][co] X[p + tap][ci]  (3x3 pad 1 / 1x1), MFMA f32
+//   snrse_conv_wgrad_x3   the same as split-bf16 products (the fp32x3 training mode)
 //   snrse_chan_sum        per-(b, c) and per-c sums of an NHWC tensor (bias / temb / GroupNorm-affine grads)
 //   snrse_gn_moments      per-(b, group) mean and rstd from the forward's slotted (sum, sumsq) statistics
 //   snrse_gn_backward     GroupNorm (+SiLU) backward: dx of one or two (channel-concatenated) sources,
@@ -89,6 +90,121 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const float* dy, int Co
         }
     }
   }
+  const int ci = ci0 + wid * 16 + ln;
+  if (ci >= Cin) return;
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int co = co0 + f * 16 + 4 * lk + e;
+      if (co >= Cout) continue;
+#pragma unroll
+      for (int t = 0; t < T; ++t) unsafeAtomicAdd(&dw[((size_t)co * T + t) * Cin + ci], acc[f][t][e]);
+    }
+}
+
+// --------------------------------------------------------------------------------------- conv wgrad, split bf16
+// The fp32x3 training mode's weight gradient: the same block / segment walk as conv_wgrad_kernel, with the
+// staged dY and X tiles split into bf16 hi / lo images in their natural [pixel][channel] layout, and each
+// 16x16x32 block as A_hi B_hi + A_hi B_lo + A_lo B_hi on v_mfma_f32_16x16x32_bf16.  The reduction axis is
+// the pixel, i.e. the ROW of both images: the operand fragments are read column-major with
+// ds_read_b64_tr_b16 (lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3; lane i receives
+// column i of the 4 rows), so a tap's pixel shift is just a row offset -- no shifted copies.
+constexpr int XW_RS = 144;  // LDS row stride (bytes): 64 bf16 + 16 B pad, a multiple of 8 for the tr reads
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+SNRSE_DEV u32x4 tr_frag(const char* img, int row0, int col) {  // k = rows row0 .. row0 + 7 of column `col`
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + row0 * XW_RS + col * 2));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (row0 + 4) * XW_RS + col * 2));
+  typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+  const u32x2 ua = __builtin_bit_cast(u32x2, a), ub = __builtin_bit_cast(u32x2, b);
+  return u32x4{ua[0], ua[1], ub[0], ub[1]};
+}
+
+SNRSE_DEV void split_store4(char* hi, char* lo, int off, const f32x4 v) {  // 4 f32 -> 4 bf16 hi + 4 bf16 lo
+  typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+  const uint32_t h01 = pack_bf16x2(v[0], v[1]), h23 = pack_bf16x2(v[2], v[3]);
+  const uint32_t l01 = pack_bf16x2(v[0] - __uint_as_float(h01 << 16), v[1] - __uint_as_float(h01 & 0xffff0000u));
+  const uint32_t l23 = pack_bf16x2(v[2] - __uint_as_float(h23 << 16), v[3] - __uint_as_float(h23 & 0xffff0000u));
+  *(u32x2*)(hi + off) = u32x2{h01, h23};
+  *(u32x2*)(lo + off) = u32x2{l01, l23};
+}
+
+template <int KS>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_x3_kernel(const float* dy, int Cout, const float* x0, int C0,
+                                                               const float* x1, int C1, int B, int H, int W,
+                                                               float* dw, int segs_per_blk) {
+  constexpr int T = KS * KS, HP = WG_P + KS - 1;
+  __shared__ __attribute__((aligned(16))) char lds[(2 * WG_P + 2 * KS * HP) * XW_RS];
+  char* const dyh = lds;
+  char* const dyl = lds + WG_P * XW_RS;
+  char* const xh = lds + 2 * WG_P * XW_RS;
+  char* const xl = xh + KS * HP * XW_RS;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64;
+  const int Cin = C0 + C1;
+  const int nws = (W + WG_P - 1) / WG_P;
+  const long long nseg = (long long)B * H * nws;
+  const long long s0 = (long long)blockIdx.z * segs_per_blk;
+  const long long s1 = std::min(nseg, s0 + segs_per_blk);
+  f32x4 acc[4][T];
+#pragma unroll
+  for (int f = 0; f < 4; ++f)
+#pragma unroll
+    for (int t = 0; t < T; ++t) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, q = (lane >> 2) & 3, cp = (lane & 3) * 4;  // tr-read group, row, column quad
+  for (long long sg = s0; sg < s1; ++sg) {
+    const int wsg = (int)(sg % nws);
+    const int h = (int)((sg / nws) % H);
+    const int b = (int)(sg / ((long long)nws * H));
+    const int w0 = wsg * WG_P;
+    __syncthreads();
+    for (int e = tid; e < WG_P * 16; e += 256) {  // dY tile [32 px][64 co], 4 channels per vector
+      const int px = e >> 4, c4 = (e & 15) * 4;
+      const int w = w0 + px, co = co0 + c4;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (w < W && co < Cout) v = *(const f32x4*)(dy + (((size_t)b * H + h) * W + w) * Cout + co);
+      split_store4(dyh, dyl, px * XW_RS + c4 * 2, v);
+    }
+    for (int e = tid; e < KS * HP * 16; e += 256) {  // X halo [KS rows][HP px][64 ci]
+      const int c4 = (e & 15) * 4, r = e >> 4;
+      const int px = r % HP, ky = r / HP;
+      const int hh = h + ky - KS / 2, ww = w0 + px - KS / 2, ci = ci0 + c4;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (hh >= 0 && hh < H && ww >= 0 && ww < W && ci < Cin) {
+        const size_t pix = ((size_t)b * H + hh) * W + ww;
+        v = ci < C0 ? *(const f32x4*)(x0 + pix * C0 + ci) : *(const f32x4*)(x1 + pix * C1 + ci - C0);
+      }
+      split_store4(xh, xl, r * XW_RS + c4 * 2, v);
+    }
+    __syncthreads();
+    u32x4 ah[4], al[4];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {  // A = dY^T: rows co, k = px
+      ah[f] = tr_frag(dyh, 8 * g + q, f * 16 + cp);
+      al[f] = tr_frag(dyl, 8 * g + q, f * 16 + cp);
+    }
+#pragma unroll
+    for (int ky = 0; ky < KS; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) {  // B = X shifted by the tap: rows px + kx of image row ky
+        const int row0 = ky * HP + 8 * g + q + kx;
+        const u32x4 bh = tr_frag(xh, row0, wid * 16 + cp), bl = tr_frag(xl, row0, wid * 16 + cp);
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          f32x4& a = acc[f][ky * KS + kx];
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, ah[f]),
+                                                      __builtin_bit_cast(bf16x8_mfma, bh), a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, ah[f]),
+                                                      __builtin_bit_cast(bf16x8_mfma, bl), a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, al[f]),
+                                                      __builtin_bit_cast(bf16x8_mfma, bh), a, 0, 0, 0);
+        }
+      }
+  }
+  const int ln = lane & 15, lk = lane >> 4;
   const int ci = ci0 + wid * 16 + ln;
   if (ci >= Cin) return;
 #pragma unroll
@@ -454,6 +570,26 @@ __global__ __launch_bounds__(256) void adam_ema_kernel(const AdamTensor* ts, con
 int grid_for(long long n) { return (int)std::min<long long>((n + 255) / 256, 65536); }
 
 }  // namespace
+
+extern "C" int snrse_conv_wgrad_x3(const float* dy, int Cout, const float* x0, int C0, const float* x1, int C1,
+                                   int B, int H, int W, int ksize, float* dw, hipStream_t s) {
+  if (!dy || !x0 || !dw || Cout <= 0 || C0 <= 0 || C1 < 0 || (C1 && !x1) || B <= 0 || H <= 0 || W <= 0 ||
+      (ksize != 1 && ksize != 3) || Cout % 4 || C0 % 4 || C1 % 4)
+    return SNRSE_EINVAL;
+  const int Cin = C0 + C1;
+  const int nci = (Cin + 63) / 64, nco = (Cout + 63) / 64;
+  const long long nseg = (long long)B * H * ((W + WG_P - 1) / WG_P);
+  long long splits = std::max<long long>(1, std::min<long long>(nseg, 2048 / (nci * nco) + 1));
+  const int per = (int)((nseg + splits - 1) / splits);
+  splits = (nseg + per - 1) / per;
+  if (ksize == 3)
+    hipLaunchKernelGGL(conv_wgrad_x3_kernel<3>, dim3(nci, nco, (unsigned)splits), dim3(256), 0, s, dy, Cout, x0, C0,
+                       x1, C1, B, H, W, dw, per);
+  else
+    hipLaunchKernelGGL(conv_wgrad_x3_kernel<1>, dim3(nci, nco, (unsigned)splits), dim3(256), 0, s, dy, Cout, x0, C0,
+                       x1, C1, B, H, W, dw, per);
+  return (int)hipGetLastError();
+}
 
 extern "C" int snrse_conv_wgrad(const float* dy, int Cout, const float* x0, int C0, const float* x1, int C1, int B,
                                 int H, int W, int ksize, float* dw, hipStream_t s) {

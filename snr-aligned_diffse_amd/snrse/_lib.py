@@ -55,6 +55,7 @@ SIGNATURES = {
     "snrse_ctx_probe_read": [_vp, _vp, _vp, _i, _vp],
     # consistency-training step (csrc/train.hip)
     "snrse_conv_wgrad": [_vp, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp],
+    "snrse_conv_wgrad_x3": [_vp, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _vp, _vp],
     "snrse_chan_sum": [_vp, _i, _i, _i, _vp, _vp, _f, _vp],
     "snrse_gn_moments": [_vp, _i, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp],
     "snrse_gn_backward": [_vp, _i, _vp, _i, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp],

@@ -100,10 +100,10 @@ def _pack(w, cin_pad, rows):
     return p.contiguous()
 
 
-# GEMM arithmetic of the training convs (forward and input-gradient): "exact" fp32 MFMA, or "x3" -- the
-# split-bf16 fp32 GEMM of the fp32x3 mode (ops.split_weight; ~2^-16 relative per product), for every conv
-# whose weight matrix has >= 128 rows (the Cout <= 16 pyramid heads and their likes stay exact).  The
-# weight gradient (snrse_conv_wgrad) is exact fp32 either way.
+# GEMM arithmetic of the training convs: "exact" fp32 MFMA, or "x3" -- the split-bf16 fp32 GEMMs of the
+# fp32x3 mode (~2^-16 relative per product): the forward and input-gradient convs whose weight matrix has
+# >= 128 rows (ops.split_weight; the Cout <= 16 pyramid heads and their likes stay exact) and every weight
+# gradient (snrse_conv_wgrad_x3).
 _GEMM = {"mode": "exact"}
 
 
@@ -168,7 +168,8 @@ class _Conv(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             cin_p = x0p.shape[-1] + (0 if x1 is None else x1.shape[-1])
             g = torch.zeros(cout, k * k, cin_p, device=dy.device, dtype=torch.float32)
-            _call("snrse_conv_wgrad", d.data_ptr(), cout, x0p.data_ptr(), x0p.shape[-1], _p(x1),
+            _call("snrse_conv_wgrad_x3" if _GEMM["mode"] == "x3" and cout % 4 == 0 else "snrse_conv_wgrad",
+                  d.data_ptr(), cout, x0p.data_ptr(), x0p.shape[-1], _p(x1),
                   0 if x1 is None else x1.shape[-1], B, H, W_, k, g.data_ptr())
             if cin_p != cin:
                 g = g[..., :cin]

@@ -236,3 +236,38 @@ def test_training_attention_vs_torch(gpu, chunked):
     for got, ref in ((o, orf), (qa.grad, qr.grad), (ka.grad, kr.grad), (va.grad, vr.grad)):
         err = (got.double() - ref).norm() / ref.norm()
         assert err < 1e-5, float(err)
+
+
+@pytest.mark.parametrize("case", [
+    # B, C0, C1, Cout, H, W, ksize
+    (2, 128, 0, 128, 16, 64, 3),
+    (1, 128, 128, 256, 8, 40, 3),   # concatenated input, W not a multiple of the 32-px segment
+    (2, 32, 0, 128, 9, 33, 3),      # the padded input conv (Cin 4 -> 32)
+    (2, 128, 0, 4, 8, 64, 3),       # a pyramid head (Cout 4)
+    (2, 256, 0, 256, 8, 16, 1),     # 1x1
+])
+def test_conv_wgrad_x3_vs_exact(gpu, case):
+    """snrse_conv_wgrad_x3 (split-bf16 products, transposed LDS reads) vs snrse_conv_wgrad (exact f32 MFMA)
+    and a float64 torch reference of the same weight gradient."""
+    import torch.nn.functional as F
+    from snrse import train as tr
+    B, C0, C1, Co, H, W, k = case
+    g = torch.Generator(device=gpu).manual_seed(sum(case))
+    x0 = torch.randn(B, H, W, C0, device=gpu, generator=g)
+    x1 = torch.randn(B, H, W, C1, device=gpu, generator=g) if C1 else None
+    dy = torch.randn(B, H, W, Co, device=gpu, generator=g)
+    Cin = C0 + C1
+    outs = {}
+    for name in ("snrse_conv_wgrad", "snrse_conv_wgrad_x3"):
+        dw = torch.zeros(Co, k * k, Cin, device=gpu)
+        tr._call(name, dy.data_ptr(), Co, x0.data_ptr(), C0, tr._p(x1), C1, B, H, W, k, dw.data_ptr())
+        torch.cuda.synchronize()
+        outs[name] = dw.reshape(Co, k, k, Cin).permute(0, 3, 1, 2).double().cpu()
+    x = x0 if x1 is None else torch.cat([x0, x1], -1)
+    xd = x.permute(0, 3, 1, 2).double().cpu()
+    dyd = dy.permute(0, 3, 1, 2).double().cpu()
+    ref = torch.nn.grad.conv2d_weight(xd, (Co, Cin, k, k), dyd, padding=k // 2)
+    def rel(a, b):
+        return float((a - b).pow(2).mean().sqrt() / b.pow(2).mean().sqrt())
+    assert rel(outs["snrse_conv_wgrad"], ref) < 1e-5
+    assert rel(outs["snrse_conv_wgrad_x3"], ref) < 3e-5
