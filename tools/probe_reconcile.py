@@ -20,7 +20,8 @@ def short(name):
     return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").split("<")[0].strip()
 
 
-CONV = ("conv_mfma_kernel", "conv_glds_kernel", "conv_halo5_kernel", "conv_head_kernel", "input_conv_kernel")
+CONV = ("conv_mfma_kernel", "conv_glds_kernel", "conv_halo5_kernel", "conv_head_kernel", "input_conv_kernel",
+        "conv_x3_kernel", "conv_x3h_kernel")
 
 
 def per_call(rows, dump):
