@@ -608,6 +608,71 @@ def upfirdn2d(inp, kernel, up=1, down=1, pad=(0, 0)):
     return out.view(N, Cc, oh, ow)
 
 
+def _upfirdn_raw(x4, k, upx, upy, dnx, dny, px0, px1, py0, py1):
+    """snrse_upfirdn2d on [major, H, W, minor] with per-axis factors and pads."""
+    major, H, W, minor = x4.shape
+    kh, kw = k.shape
+    oh = (H * upy + py0 + py1 - kh) // dny + 1
+    ow = (W * upx + px0 + px1 - kw) // dnx + 1
+    out = torch.empty(major, oh, ow, minor, device=x4.device, dtype=x4.dtype)
+    dt = UPFIRDN_DTYPES.get(x4.dtype)
+    if dt is None:
+        raise TypeError(f"upfirdn2d: unsupported dtype {x4.dtype} (float, double, half, bfloat16)")
+    _lib.call("snrse_upfirdn2d", x4.contiguous().data_ptr(), out.data_ptr(), k.to(torch.float32).contiguous().data_ptr(),
+              major, H, W, minor, kh, kw, upx, upy, dnx, dny, px0, px1, py0, py1, dt, _stream())
+    return out
+
+
+class _UpFirDn2d(torch.autograd.Function):
+    """upfirdn2d with gradients, every direction through snrse_upfirdn2d -- the call pattern of the
+    reference's UpFirDn2d / UpFirDn2dBackward (op/upfirdn2d.py:19-142): the input gradient is the op on
+    the output gradient with the flipped kernel, up and down swapped and the transposed pads
+    (kw - pad_x0 - 1, in_w up - out_w down + pad_x0 - up + 1, likewise in y); its own gradient is the
+    forward op again."""
+
+    @staticmethod
+    def forward(ctx, x, kernel, up, down, pad):
+        (upx, upy), (dnx, dny), (px0, px1, py0, py1) = up, down, pad
+        N, C, H, W = x.shape
+        kh, kw = kernel.shape
+        out = _upfirdn_raw(x.reshape(N * C, H, W, 1), kernel, upx, upy, dnx, dny, px0, px1, py0, py1)
+        oh, ow = out.shape[1], out.shape[2]
+        ctx.save_for_backward(kernel)
+        ctx.geom = (up, down, pad, (N, C, H, W), (oh, ow),
+                    (kw - px0 - 1, W * upx - ow * dnx + px0 - upx + 1, kh - py0 - 1, H * upy - oh * dny + py0 - upy + 1))
+        return out.view(N, C, oh, ow)
+
+    @staticmethod
+    def backward(ctx, g):
+        (kernel,) = ctx.saved_tensors
+        return _UpFirDn2dGrad.apply(g, kernel, ctx.geom), None, None, None, None
+
+
+class _UpFirDn2dGrad(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, g, kernel, geom):
+        (upx, upy), (dnx, dny), _, (N, C, H, W), (oh, ow), (gx0, gx1, gy0, gy1) = geom
+        gi = _upfirdn_raw(g.contiguous().reshape(N * C, oh, ow, 1), torch.flip(kernel, [0, 1]), dnx, dny, upx, upy,
+                          gx0, gx1, gy0, gy1)
+        ctx.save_for_backward(kernel)
+        ctx.geom = geom
+        return gi.view(N, C, H, W)
+
+    @staticmethod
+    def backward(ctx, gg):
+        (kernel,) = ctx.saved_tensors
+        (upx, upy), (dnx, dny), (px0, px1, py0, py1), (N, C, H, W), (oh, ow), _ = ctx.geom
+        go = _upfirdn_raw(gg.contiguous().reshape(N * C, H, W, 1), kernel, upx, upy, dnx, dny, px0, px1, py0, py1)
+        return go.view(N, C, oh, ow), None, None
+
+
+def upfirdn2d_autograd(inp, kernel, up=1, down=1, pad=(0, 0)):
+    """The reference's upfirdn2d(input, kernel, up, down, pad) (op/upfirdn2d.py:145-156) with its autograd
+    (first and second derivatives w.r.t. the input), on the HIP op."""
+    _dev(inp, kernel)
+    return _UpFirDn2d.apply(inp, kernel, (up, up), (down, down), (pad[0], pad[1], pad[0], pad[1]))
+
+
 def set_option(name: str, value: int):
     """Process-wide switch: the library's process default context and every live LaunchContext."""
     _lib.call("snrse_set_option", name.encode(), int(value))

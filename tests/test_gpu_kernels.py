@@ -184,6 +184,44 @@ def test_upfirdn2d_reference_api(gpu):
     np.testing.assert_allclose(nchw(ops.fir(nhwc(x), "down")).cpu().numpy(), g["down"], atol=1e-5)
 
 
+@pytest.mark.parametrize("up,down,pad", [(2, 1, (2, 1)), (1, 2, (1, 1)), (1, 1, (1, 2)), (2, 2, (1, 2))])
+def test_upfirdn2d_gradients(gpu, up, down, pad):
+    """Gradients through the HIP op in the reference's autograd call pattern (ops.upfirdn2d_autograd: the
+    input gradient is snrse_upfirdn2d on the output gradient with the flipped kernel, up / down swapped and
+    the transposed pads; the gradient of that w.r.t. the output gradient is the forward op again) vs a
+    float64 restatement (zero-insert, pad, conv2d with the flipped kernel, subsample) and its torch autograd."""
+    from snrse import ops
+    k = torch.tensor([1.0, 3.0, 3.0, 1.0], dtype=torch.float64)
+    k2 = torch.outer(k, k)
+    k2 = k2 / k2.sum() * (up * up)
+
+    def native(x):
+        N, C, H, W = x.shape
+        u = x.new_zeros(N, C, H * up, W * up)
+        u[:, :, ::up, ::up] = x
+        u = F.pad(u, (pad[0], pad[1], pad[0], pad[1]))
+        w = torch.flip(k2, [0, 1]).to(x.dtype).expand(C, 1, 4, 4)
+        return F.conv2d(u, w, groups=C)[:, :, ::down, ::down]
+
+    x = torch.from_numpy(fnormal("t.ufd.x", (2, 3, 12, 20))).double()
+    y_ref = native(x)
+    gy = torch.from_numpy(fnormal("t.ufd.gy", tuple(y_ref.shape))).double()
+    v = torch.from_numpy(fnormal("t.ufd.v", tuple(x.shape))).double()
+    xr = x.clone().requires_grad_(True)
+    (g_ref,) = torch.autograd.grad(native(xr), xr, gy)
+    kg = k2.float().to(gpu)
+    xg = x.float().to(gpu).requires_grad_(True)
+    gyg = gy.float().to(gpu).requires_grad_(True)
+    y = ops.upfirdn2d_autograd(xg, kg, up=up, down=down, pad=pad)
+    assert y.shape == y_ref.shape
+    np.testing.assert_allclose(y.detach().double().cpu().numpy(), y_ref.numpy(), atol=1e-5)
+    (g,) = torch.autograd.grad(y, xg, gyg, create_graph=True)
+    np.testing.assert_allclose(g.detach().double().cpu().numpy(), g_ref.numpy(), atol=1e-5)
+    # <g, v> = <gy, op(v)>: its gradient w.r.t. the output gradient is the forward op on v
+    (d_gy,) = torch.autograd.grad(g, gyg, v.float().to(gpu))
+    np.testing.assert_allclose(d_gy.double().cpu().numpy(), native(v).numpy(), atol=1e-5)
+
+
 @pytest.mark.parametrize("dtype,atol", [(torch.float64, 1e-12), (torch.float16, 4e-3)])
 def test_upfirdn2d_half_double(gpu, dtype, atol):
     """The reference binding's other element types (AT_DISPATCH_FLOATING_TYPES_AND_HALF,
