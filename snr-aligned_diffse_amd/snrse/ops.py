@@ -185,7 +185,10 @@ def conv2d(src0, wgt, ksize, cout, bias=None, src1=None, sc=None, sc1=None, sc_w
     return out
 
 
-_VARIANT = {"v": 0, "x3_tile": 0}
+def _opt(x, name):
+    """A library switch as the launch context of x's device sees it (set_option, SNRSE_OPTS or a
+    per-context setting): the shape predicates below mirror the library's own dispatch."""
+    return context(x.device).get_option(name)
 
 
 def get_option(name):
@@ -248,7 +251,7 @@ def halo_ok(x, ksize, cout):
     # images tileable by 4 x 64 (the kernel then uses 8 x 32 tiles where H % 8 == 0); W = 32 alone stays on
     # the split-K GEMM (faster there: profiles/r03v_level4_halo_vs_glds.jsonl)
     return (x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and H % 4 == 0 and W % 64 == 0
-            and _VARIANT["v"] in (0, 5))
+            and _opt(x, "conv_variant") in (0, 5))
 
 
 def x3h_ok(x, ksize, cout):
@@ -259,7 +262,7 @@ def x3h_ok(x, ksize, cout):
     B, H, W, C = x.shape
     if x.dtype != torch.float32 or ksize != 3 or cout % 128 or H % 4:
         return False
-    t = _VARIANT["x3_tile"]
+    t = _opt(x, "x3_tile")
     return t == 4 or (t == 0 and B * (H // 4) * (-(-W // 64)) * (cout // 128) >= 256)
 
 
@@ -267,7 +270,8 @@ def head_ok(x):
     """True when a bf16 3x3 conv of x with Cout <= 16 and f32 output (the pyramid heads) takes the
     halo-staged head kernel, which accepts a fused GroupNorm (gn=)."""
     B, H, W, C = x.shape
-    return x.dtype == torch.bfloat16 and H % 8 == 0 and W % 32 == 0 and C % 32 == 0 and _VARIANT["v"] != 1
+    return (x.dtype == torch.bfloat16 and H % 8 == 0 and W % 32 == 0 and C % 32 == 0
+            and _opt(x, "conv_variant") != 1)
 
 
 def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):
@@ -678,10 +682,6 @@ def set_option(name: str, value: int):
     _lib.call("snrse_set_option", name.encode(), int(value))
     for c in list(_CONTEXTS):
         c.set_option(name, value)
-    if name == "conv_variant":
-        _VARIANT["v"] = int(value)
-    if name == "x3_tile":
-        _VARIANT["x3_tile"] = int(value)
 
 
 def spec_transform(spec, direction):
