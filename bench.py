@@ -560,6 +560,37 @@ def run(args):
             parity["tol_abs"] = 1e-4
             parity["ok"] = bool(parity["ok"] and r["abs_rms"] < 1e-4)
 
+    # The same C2 workload in the fp32x3 parity mode (split-bf16 fp32 GEMMs: within the north star's 1e-4
+    # RMS) beside the bf16 headline, single-GPU default runs only: one warm-up and one timed step, then its
+    # own N=5 PC golden check (halo kernel forced at the golden's size)
+    pmode = None
+    if (world == 1 and args.config == "c2" and args.dtype == "bf16" and not args.no_parity_mode
+            and args.seconds == 4.0 and args.N == 30):
+        del enh, probe_enh, net
+        torch.cuda.empty_cache()
+        net3 = ncsnpp.NCSNppHIP(formula_weights(), dtype=torch.float32, device=dev, gemm="x3")
+        enh3 = PCEnhancer(net3, sde, N=args.N)
+        enh3(y, noise(50))
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        enh3(y, noise(150))
+        torch.cuda.synchronize()
+        el3 = time.perf_counter() - t3
+        pmode = {"dtype": "fp32x3", "value": B / el3, "unit": "utt/s", "ms_per_step": el3 * 1e3, "steps": 1,
+                 "warmup": 1, "note": ("fp32 activations / storage / accumulation, ResBlock and input convs as "
+                                       "split-bf16 GEMMs (bench.py --dtype fp32x3 for the full line)")}
+        if not args.no_parity:
+            import paritycheck
+            ops.set_option("x3_tile", 4)
+            try:
+                r3 = paritycheck.pc_vs_golden(dev, net3)
+            finally:
+                ops.set_option("x3_tile", 0)
+            pmode["parity"] = {"abs_rms": r3["abs_rms"], "rel_rms": r3["rel_rms"], "tol_abs": 1e-4,
+                               "ok": bool(r3["ok"] and r3["abs_rms"] < 1e-4), "golden": "tests/golden/pc_ouve.npz"}
+        del enh3, net3
+        torch.cuda.empty_cache()
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         cpu = cpu_baseline()
@@ -597,6 +628,8 @@ def run(args):
             "roofline": roof, "cpu_baseline": cpu, "parity": parity,
             "output_rms_mean": float(allm.mean()),
         }
+        if pmode is not None:
+            line["parity_mode"] = pmode
         if sdist.oversubscribed(world):  # a launcher rehearsal: ranks share the visible GPU(s)
             line["oversubscribed"] = {"ranks": world, "devices": torch.cuda.device_count(),
                                       "note": "ranks share devices; collectives on gloo; not a scaling figure"}
@@ -623,6 +656,8 @@ def main():
                     help="bf16; fp32 (exact fp32 MFMA GEMMs); fp32x3 (fp32 activations, split-bf16 GEMMs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
+    ap.add_argument("--no-parity-mode", action="store_true",
+                    help="skip the fp32x3 parity-mode step timed beside the default bf16 C2 line")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the post-run parity check of the benched network vs tests/golden/pc_ouve.npz")
     ap.add_argument("--conv-variant", type=int, default=0, help="snrse conv_variant option (0 = auto)")
