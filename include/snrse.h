@@ -117,13 +117,14 @@ int snrse_gn_apply(const void* src0, int C0, const void* src1, int C1, int B, in
                    const double* sums, const double* sums1, const float* gamma, const float* beta,
                    int groups, float eps, int act, int mode, void* out, int dtype, hipStream_t stream);
 
-/* LDS-tiled GroupNorm-apply + SiLU + FIR x2 of a ResBlock with up/down (layerspp.py:245-257), bf16:
+/* LDS-tiled GroupNorm-apply + SiLU + FIR x2 of a ResBlock with up/down (layerspp.py:245-257):
  * out_act = FIR(act(x*scale+shift)) and, when out_raw != NULL, out_raw = FIR(x) (the shortcut input,
  * layerspp.py:249/255), both [B][Ho][Wo][C] from one pass over x.  scale/shift [B][C] f32 from
- * snrse_gn_scale_shift, or both NULL (identity).  mode 1 down (H, W even), 2 up.  C % 8 == 0 with C / 8
- * dividing 64 (the row-strip kernel), otherwise C % 16 == 0 (the LDS-tiled kernel). */
+ * snrse_gn_scale_shift, or both NULL (identity).  mode 1 down (H, W even), 2 up.  dtype SNRSE_BF16: C % 8 == 0
+ * with C / 8 dividing 64 (the row-strip kernel), otherwise C % 16 == 0 (the LDS-tiled kernel); SNRSE_F32
+ * (the fp32 parity modes): C % 4 == 0 with C / 4 dividing 64 (row strips). */
 int snrse_gn_resample(snrse_ctx* ctx, const void* src, int C, int B, int H, int W, const float* scale, const float* shift,
-                      int act, int mode, void* out_act, void* out_raw, hipStream_t stream);
+                      int act, int mode, void* out_act, void* out_raw, int dtype, hipStream_t stream);
 
 /* Elementwise GroupNorm-apply (+SiLU) of the channel concatenation (src0 | src1), dtype SNRSE_BF16 or
  * SNRSE_F32 (exact SiLU), from precomputed scale/shift [B][C0+C1] (snrse_gn_scale_shift; both NULL:

@@ -1,6 +1,7 @@
 // LDS-tiled GroupNorm-apply + SiLU + FIR [1,3,3,1] down/up-sampling, and the elementwise
 // GroupNorm-apply (+ SiLU) over a channel concatenation, both from precomputed per-(b, c)
-// scale / shift (snrse_gn_scale_shift).  bf16 storage, f32 arithmetic (gfx950).
+// scale / shift (snrse_gn_scale_shift).  bf16 storage (the row-strip kernel also f32), f32 arithmetic
+// (gfx950).
 //
 // Reference ops replaced (BigGAN ResBlock with up / down, layerspp.py:245-268):
 //   h = act(GroupNorm_0(x)); h = upsample_2d / downsample_2d(h, fir_kernel)   (:245-257)
@@ -260,14 +261,15 @@ __global__ __launch_bounds__(256) void gn_act_kernel(const T* __restrict__ src0,
 //         (3 V(q) + V(q+1)) / 4
 // Zero padding applies to the activated tensor and to x (out-of-image vectors are 0 for both).
 
-template <int CPT> struct RVec;  // CPT channels of one pixel: 16 B (8 ch) or 8 B (4 ch)
-template <> struct RVec<8> {
+// CPT channels of one pixel: bf16 16 B (8 ch) or 8 B (4 ch); f32 16 B (4 ch)
+template <typename E, int CPT> struct RVec;
+template <> struct RVec<bf16_t, 8> {
   typedef u32x4 T;
   SNRSE_DEV static T load(__amdgpu_buffer_rsrc_t r, int off) { return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0); }
   SNRSE_DEV static void unpack(const T v, float* x) { unpack8(v, x); }
   SNRSE_DEV static T pack(const float* x) { return pack8(x); }
 };
-template <> struct RVec<4> {
+template <> struct RVec<bf16_t, 4> {
   typedef __attribute__((ext_vector_type(2))) unsigned int T;
   SNRSE_DEV static T load(__amdgpu_buffer_rsrc_t r, int off) { return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0); }
   SNRSE_DEV static void unpack(const T v, float* x) {
@@ -278,6 +280,17 @@ template <> struct RVec<4> {
     }
   }
   SNRSE_DEV static T pack(const float* x) { return T{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])}; }
+};
+template <> struct RVec<float, 4> {
+  typedef u32x4 T;
+  SNRSE_DEV static T load(__amdgpu_buffer_rsrc_t r, int off) { return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0); }
+  SNRSE_DEV static void unpack(const T v, float* x) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = __uint_as_float(v[i]);
+  }
+  SNRSE_DEV static T pack(const float* x) {
+    return T{__float_as_uint(x[0]), __float_as_uint(x[1]), __float_as_uint(x[2]), __float_as_uint(x[3])};
+  }
 };
 
 template <int CPT> struct RowVec {  // act and raw values of one CPT-channel vector
@@ -298,14 +311,14 @@ SNRSE_DEV __amdgpu_buffer_rsrc_t rs_rsrc(const void* base, unsigned bytes) {
 // RD (down only): output rows per strip.  A strip of RD rows reads 2 RD + 2 input rows, so each input
 // vector's GroupNorm + SiLU is evaluated (2 RD + 2) / RD times instead of 4 (the kernel's VALU) and each
 // input row is fetched by fewer strips (L2 traffic).
-template <int MODE, int NV, int CPT, int RD = 1>
-__global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __restrict__ src, int H, int W, int L,
+template <typename E, int MODE, int NV, int CPT, int RD = 1>
+__global__ __launch_bounds__(256) void gn_resample_rows_kernel(const E* __restrict__ src, int H, int W, int L,
                                                                int nseg, int nrows, const float* __restrict__ scale,
                                                                const float* __restrict__ shift, int act,
-                                                               bf16_t* __restrict__ out_act,
-                                                               bf16_t* __restrict__ out_raw, int nblk, int B,
+                                                               E* __restrict__ out_act,
+                                                               E* __restrict__ out_raw, int nblk, int B,
                                                                int sp_img, int nt) {
-  using V = RVec<CPT>;
+  using V = RVec<E, CPT>;
   constexpr int C = NV * CPT, SPB = 256 / NV;  // strips per block
   // XCD-aware bijective remap: consecutive logical blocks (neighbouring output rows, which share input
   // rows) run on one XCD and its L2
@@ -328,7 +341,7 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
     sc[i] = (scale ? scale[(size_t)b * C + CPT * v + i] : 1.f) * pre;
     sh[i] = (scale ? shift[(size_t)b * C + CPT * v + i] : 0.f) * pre;
   }
-  const __amdgpu_buffer_rsrc_t rsrc = rs_rsrc(src + (size_t)b * H * W * C, (unsigned)((size_t)H * W * C * 2));
+  const __amdgpu_buffer_rsrc_t rsrc = rs_rsrc(src + (size_t)b * H * W * C, (unsigned)((size_t)H * W * C * sizeof(E)));
   constexpr int NR = MODE == MODE_DOWN ? 2 * RD + 2 : 2;  // input rows of the strip's RD output rows
   int iy0;
   float wy[NR];
@@ -357,7 +370,7 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
 #pragma unroll
     for (int a = 0; a < NR; ++a) {
       const bool ok = colok && rowok[a];
-      rw.x[a] = V::load(rsrc, ok ? (((iy0 + a) * W + ix) * C + CPT * v) * 2 : (int)0x80000000);  // outside: 0
+      rw.x[a] = V::load(rsrc, ok ? (((iy0 + a) * W + ix) * C + CPT * v) * (int)sizeof(E) : (int)0x80000000);  // outside: 0
     }
     return rw;
   };
@@ -500,7 +513,7 @@ __global__ __launch_bounds__(256) void gn_resample_rows_kernel(const bf16_t* __r
   }
 }
 
-template <int MODE, int NV, int CPT, int RD = 1>
+template <typename E, int MODE, int NV, int CPT, int RD = 1>
 int launch_rows(const void* src, int B, int H, int W, const float* scale, const float* shift, int act, void* out_act,
                 void* out_raw, hipStream_t stream, int nt) {
   const int nrows = MODE == MODE_DOWN ? H / 2 / RD : 2 * H;  // strips per column segment
@@ -513,50 +526,62 @@ int launch_rows(const void* src, int B, int H, int W, const float* scale, const 
   constexpr int SPB = 256 / NV, SPW = 64 / NV;
   const long long sp_img = ((long long)nrows * nseg + SPW - 1) / SPW * SPW;  // strips per image, padded
   const long long nblk = (sp_img * B + SPB - 1) / SPB;
-  if (nblk > 0x7fffffffLL || sp_img * B > 0x7fffffffLL || (long long)H * W * NV * CPT * 2 >= 0x7fffffffLL)
+  if (nblk > 0x7fffffffLL || sp_img * B > 0x7fffffffLL ||
+      (long long)H * W * NV * CPT * (long long)sizeof(E) >= 0x7fffffffLL)
     return SNRSE_EINVAL;
-  hipLaunchKernelGGL((gn_resample_rows_kernel<MODE, NV, CPT, RD>), dim3((unsigned)nblk), dim3(256), 0, stream,
-                     (const bf16_t*)src, H, W, L, nseg, nrows, scale, shift, act, (bf16_t*)out_act, (bf16_t*)out_raw,
-                     (int)nblk, B, (int)sp_img, nt);
+  hipLaunchKernelGGL((gn_resample_rows_kernel<E, MODE, NV, CPT, RD>), dim3((unsigned)nblk), dim3(256), 0, stream,
+                     (const E*)src, H, W, L, nseg, nrows, scale, shift, act, (E*)out_act, (E*)out_raw, (int)nblk, B,
+                     (int)sp_img, nt);
   return (int)hipGetLastError();
 }
 
-// down: 4 channels per lane (8 input vectors per output column pair stay within 4 waves per SIMD);
-// up: 8 channels per lane (16-B stores)
-template <int MODE, int RD>
+// bf16 down: 4 channels per lane (8 input vectors per output column pair stay within 4 waves per SIMD);
+// bf16 up: 8 channels per lane (16-B stores); f32: 4 channels per lane (16 B) both ways
+template <typename E, int MODE, int RD>
 int dispatch_rows_rd(const void* src, int C, int B, int H, int W, const float* scale, const float* shift, int act,
                      void* out_act, void* out_raw, hipStream_t stream, int nt) {
-  constexpr int CPT = MODE == MODE_DOWN ? 4 : 8;
+  constexpr int CPT = sizeof(E) == 4 ? 4 : (MODE == MODE_DOWN ? 4 : 8);
   if (C % CPT) return -1;
   switch (C / CPT) {
-    case 1: return launch_rows<MODE, 1, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
-    case 2: return launch_rows<MODE, 2, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
-    case 4: return launch_rows<MODE, 4, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
-    case 8: return launch_rows<MODE, 8, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
-    case 16: return launch_rows<MODE, 16, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
-    case 32: return launch_rows<MODE, 32, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
-    case 64: return launch_rows<MODE, 64, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
+#define SNRSE_RS_NV(N) \
+  case N: return launch_rows<E, MODE, N, CPT, RD>(src, B, H, W, scale, shift, act, out_act, out_raw, stream, nt);
+    SNRSE_RS_NV(1)
+    SNRSE_RS_NV(2)
+    SNRSE_RS_NV(4)
+    SNRSE_RS_NV(8)
+    SNRSE_RS_NV(16)
+    SNRSE_RS_NV(32)
+    SNRSE_RS_NV(64)
+#undef SNRSE_RS_NV
     default: return -1;  // not handled here
   }
 }
-template <int MODE>
+// down strips of 4 output rows (bf16 default) hold 10 input vectors per column in flight; f32 vectors
+// are twice the registers, so f32 strips stop at 2 rows
+template <typename E, int MODE>
 int dispatch_rows(const void* src, int C, int B, int H, int W, const float* scale, const float* shift, int act,
                   void* out_act, void* out_raw, hipStream_t stream, const snrse_ctx& cx) {
   if constexpr (MODE == MODE_DOWN) {
     const int Ho = H / 2;
-    if (cx.resample_down_rows >= 4 && Ho % 4 == 0)
-      return dispatch_rows_rd<MODE, 4>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx.resample_nt);
+    if constexpr (sizeof(E) == 2)
+      if (cx.resample_down_rows >= 4 && Ho % 4 == 0)
+        return dispatch_rows_rd<E, MODE, 4>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream,
+                                            cx.resample_nt);
     if (cx.resample_down_rows >= 2 && Ho % 2 == 0)
-      return dispatch_rows_rd<MODE, 2>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx.resample_nt);
+      return dispatch_rows_rd<E, MODE, 2>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx.resample_nt);
   }
-  return dispatch_rows_rd<MODE, 1>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx.resample_nt);
+  return dispatch_rows_rd<E, MODE, 1>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx.resample_nt);
 }
 
 template <int MODE>
 int launch_resample(const void* src, int C, int B, int H, int W, const float* scale, const float* shift, int act,
-                    void* out_act, void* out_raw, hipStream_t stream, const snrse_ctx& cx) {
+                    void* out_act, void* out_raw, int dtype, hipStream_t stream, const snrse_ctx& cx) {
+  if (dtype == SNRSE_F32) {  // the row-strip kernel only (C / 4 dividing 256)
+    const int r = dispatch_rows<float, MODE>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx);
+    return r >= 0 ? r : SNRSE_EINVAL;
+  }
   if (cx.resample_variant == 0) {
-    const int r = dispatch_rows<MODE>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx);
+    const int r = dispatch_rows<bf16_t, MODE>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx);
     if (r >= 0) return r;
   }
   if (C % kCB) return SNRSE_EINVAL;
@@ -573,16 +598,18 @@ int launch_resample(const void* src, int C, int B, int H, int W, const float* sc
 }  // namespace
 
 extern "C" int snrse_gn_resample(snrse_ctx* ctx, const void* src, int C, int B, int H, int W, const float* scale,
-                                 const float* shift, int act, int mode, void* out_act, void* out_raw,
+                                 const float* shift, int act, int mode, void* out_act, void* out_raw, int dtype,
                                  hipStream_t stream) {
-  if (!src || !out_act || C <= 0 || C % 8 || B <= 0 || H <= 0 || W <= 0 || (!scale) != (!shift))
+  if (!src || !out_act || C <= 0 || C % (dtype == SNRSE_F32 ? 4 : 8) || B <= 0 || H <= 0 || W <= 0 ||
+      (!scale) != (!shift) || (dtype != SNRSE_BF16 && dtype != SNRSE_F32))
     return SNRSE_EINVAL;
+  const snrse_ctx& cx = *snrse_ctx_resolve(ctx);
   if (mode == MODE_DOWN) {
     if ((H & 1) || (W & 1)) return SNRSE_EINVAL;
-    return launch_resample<MODE_DOWN>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, *snrse_ctx_resolve(ctx));
+    return launch_resample<MODE_DOWN>(src, C, B, H, W, scale, shift, act, out_act, out_raw, dtype, stream, cx);
   }
   if (mode == MODE_UP)
-    return launch_resample<MODE_UP>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, *snrse_ctx_resolve(ctx));
+    return launch_resample<MODE_UP>(src, C, B, H, W, scale, shift, act, out_act, out_raw, dtype, stream, cx);
   return SNRSE_EINVAL;
 }
 

@@ -44,7 +44,7 @@ SIGNATURES = {
     "snrse_spec_transform": [_vp, _vp, C.c_longlong, _i, _vp],
     "snrse_snrnet": [_vp, _i, _i] + [_vp] * 17 + [_vp, _vp, _vp],
     "snrse_istft": [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp],
-    "snrse_gn_resample": [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp],
+    "snrse_gn_resample": [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _i, _vp],
     "snrse_gn_act": [_vp, _i, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _i, _vp],
     "snrse_set_workspace": [_vp, C.c_size_t],
     # caller-owned launch contexts (snrse_ctx: switches, split-K workspace, read-backs)

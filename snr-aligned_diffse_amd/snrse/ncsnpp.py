@@ -217,7 +217,7 @@ class NCSNppHIP:
             gn0 = ops.gn_scale_shift(s0, e["gn0_g"], e["gn0_b"], H * W, sums1=s1)
             h, hs_ = self._conv(t0, e["w0"], 3, m.cout, src1=t1, gn=gn0, bias=e["b0"], temb=dense,
                                 temb_off=e["temb_off"])
-        elif mode != "none" and t1 is None and t0.dtype == torch.bfloat16 and t0.shape[3] % 16 == 0:
+        elif mode != "none" and t1 is None and ops.resample_ok(t0):
             # one LDS-tiled pass: SiLU(GN(x)) resampled for Conv_0 and the raw FIR of x for Conv_2
             gn0 = ops.gn_scale_shift(s0, e["gn0_g"], e["gn0_b"], H * W)
             a0, xs_raw = ops.gn_resample(t0, *gn0, act=True, mode=mode, want_raw="w2" in e)

@@ -396,13 +396,13 @@ def gn_apply(src0, src1=None, sums=None, gamma=None, beta=None, act=True, mode="
     C1 = 0 if src1 is None else src1.shape[3]
     C = C0 + C1
     m = MODES[mode]
-    if sums is not None and (m == 0 or src0.dtype == torch.bfloat16):
+    if sums is not None and (m == 0 or resample_ok(src0)):
         # the per-(b, c) affine once (snrse_gn_scale_shift), then the elementwise / LDS-tiled apply: no
         # per-block re-fold of the slotted statistics (the fp32 gn_apply pass ran at ~0.2 of HBM peak that way)
         scale, shift = gn_scale_shift(sums, gamma, beta, H * W, sums1=sums1, groups=groups, eps=eps)
         if m == 0:
             return gn_act(src0, src1, scale, shift, act=act)
-        if src1 is None and C0 % 16 == 0:
+        if src1 is None and resample_ok(src0):
             return gn_resample(src0, scale, shift, act=act, mode=mode)[0]
     Ho, Wo = (H // 2, W // 2) if m == 1 else ((2 * H, 2 * W) if m == 2 else (H, W))
     out = torch.empty(B, Ho, Wo, C, device=src0.device, dtype=src0.dtype)
@@ -412,13 +412,22 @@ def gn_apply(src0, src1=None, sums=None, gamma=None, beta=None, act=True, mode="
     return out
 
 
+def resample_ok(x):
+    """True when snrse_gn_resample takes x (NHWC): bf16 with C % 16 == 0, or f32 with C / 4 dividing 64."""
+    C = x.shape[3]
+    if x.dtype == torch.bfloat16:
+        return C % 16 == 0
+    return x.dtype == torch.float32 and C % 4 == 0 and 64 % (C // 4) == 0
+
+
 def gn_resample(x, scale=None, shift=None, act=True, mode="down", want_raw=False):
     """act(x*scale+shift) FIR-resampled x2 ('down' / 'up': upfirdn2d with [1,3,3,1]) and, with
     want_raw, the FIR of x itself (the ResBlock shortcut input) from one LDS-tiled pass over x
-    (snrse_gn_resample; bf16, C % 8 == 0 with C / 8 dividing 64, or C % 16 == 0).  Returns (activated, raw or None)."""
+    (snrse_gn_resample; bf16: C % 8 == 0 with C / 8 dividing 64, or C % 16 == 0; f32: C / 4 dividing 64).
+    Returns (activated, raw or None)."""
     _dev(x, scale, shift)
-    if x.dtype != torch.bfloat16:
-        raise TypeError("snrse: gn_resample takes bf16 activations")
+    if x.dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError("snrse: gn_resample takes bf16 or f32 activations")
     B, H, W, C = x.shape
     m = MODES[mode]
     if m == 0:
@@ -427,7 +436,7 @@ def gn_resample(x, scale=None, shift=None, act=True, mode="down", want_raw=False
     oa = torch.empty(B, Ho, Wo, C, device=x.device, dtype=x.dtype)
     orw = torch.empty_like(oa) if want_raw else None
     _lib.call("snrse_gn_resample", _cx(x.device), x.data_ptr(), C, B, H, W, _ptr(scale), _ptr(shift), int(bool(act)), m,
-              oa.data_ptr(), _ptr(orw), _stream())
+              oa.data_ptr(), _ptr(orw), code(x.dtype), _stream())
     return oa, orw
 
 

@@ -535,6 +535,42 @@ def test_gn_resample_tiled(gpu, mode, shape, variant):
     assert rel(nchw(r.float()), ref_r) < 1e-2
 
 
+@pytest.mark.parametrize("rows", [1, 2])
+@pytest.mark.parametrize("mode", ["down", "up"])
+@pytest.mark.parametrize("shape", [(2, 128, 8, 16), (1, 256, 36, 70), (3, 16, 18, 34), (1, 32, 9, 21),
+                                   (2, 128, 64, 256), (2, 4, 8, 8)])
+def test_gn_resample_f32(gpu, mode, shape, rows):
+    """The row-strip GroupNorm+SiLU+FIR kernel on f32 activations (the fp32 parity modes' up / down
+    ResBlocks, layerspp.py:245-257): activated and raw outputs against the oracle FIR of an fp64
+    GroupNorm+SiLU, to f32 accuracy; down strips of 1 and 2 output rows."""
+    from snrse import ops
+    B, C, H, W = shape
+    if mode == "down" and (H % 2 or W % 2):
+        pytest.skip("down-sampling needs even H and W")
+    x = torch.from_numpy(fnormal("t.rsf.x", (B, C, H, W))) * 2 + 0.3
+    g = torch.from_numpy(fnormal("t.rsf.g", (C,))) * 0.1 + 1
+    be = torch.from_numpy(fnormal("t.rsf.b", (C,))) * 0.1
+    fir = ncsnpp_ref.fir_down2 if mode == "down" else ncsnpp_ref.fir_up2
+    ref_a = fir(F.silu(F.group_norm(x.double(), min(C // 4, 32), g.double(), be.double(), eps=1e-6)))
+    ref_r = fir(x.double())
+    xg = nhwc(x).to(gpu, torch.float32)
+    assert ops.resample_ok(xg)
+    sums, _ = ops.gn_stats(xg)
+    scale, shift = ops.gn_scale_shift(sums, g.to(gpu), be.to(gpu), H * W)
+    old = ops.get_option("resample_down_rows")
+    ops.set_option("resample_down_rows", rows)
+    try:
+        a, r = ops.gn_resample(xg, scale, shift, act=True, mode=mode, want_raw=True)
+    finally:
+        ops.set_option("resample_down_rows", old)
+    assert a.dtype == torch.float32 and r.dtype == torch.float32
+    assert rel(nchw(a), ref_a) < 2e-6
+    assert rel(nchw(r), ref_r) < 2e-6
+    # gn_apply routes f32 up / down through the same kernel
+    ga = ops.gn_apply(xg, None, sums, g.to(gpu), be.to(gpu), act=True, mode=mode)
+    assert rel(nchw(ga), ref_a) < 2e-6
+
+
 @pytest.mark.parametrize("case", ["bf16", "bf16_f32out", "f32"])
 def test_conv_splitk_small_levels(gpu, case):
     """Small-image convs (the tile grid underfills the CUs) run as split-K GEMMs whose fp32 partial
