@@ -88,7 +88,9 @@ int snrse_upfirdn2d(const void* in, void* out, const float* kernel, int major, i
  *   dtype SNRSE_F32X3: src/res/out fp32; wgt [Npad][2*ksize*ksize*(C0+C1)] and sc_wgt [Npad][2*(Csc+Csc1)]
  *          bf16, each 32-element K-tile of the fp32 packing stored as 32 hi = bf16(w) then 32
  *          lo = bf16(w - hi); Cout % 128 == 0 or Cout <= 16 (Npad 16); gn_scale only on the halo form
- *          (3x3, H % 4 == 0, >= 256 tiles or option x3_tile 4), else hipErrorInvalidValue; out_f32 ignored. */
+ *          (3x3, H % 4 == 0, >= 256 tiles or option x3_tile 4) and the pyramid head (3x3, Cout <= 16,
+ *          H % 8 == 0, W % 32 == 0, C0 / C1 % 32 == 0, no stats / temb / shortcut / combine), else
+ *          hipErrorInvalidValue; out_f32 ignored. */
 int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void* src1, int C1, int B, int H, int W, int ksize,
                  const void* wgt, const void* sc_src, int Csc, const void* sc_src1, int Csc1,
                  const void* sc_wgt, const float* bias, const float* temb, int temb_stride,
@@ -157,7 +159,7 @@ int snrse_set_option(const char* name, int value);
 
 /* Read back a switch (any name above) or: "halo_kernel" = generation of the halo conv kernel the current
  * setting dispatches to (5), "last_kernel" = generation of the most recent snrse_conv2d launch (1 v1, 2 v2,
- * 5 halo, 10 pyramid head), "last_ksplit" = K splits of the most recent v2 launch, "last_epi_nt" /
+ * 3 / 4 split-bf16 register-staged / halo, 5 halo, 10 pyramid head, 11 split-bf16 pyramid head), "last_ksplit" = K splits of the most recent v2 launch, "last_epi_nt" /
  * "last_chunks" = store flavour / image-range launches of the most recent halo conv, "last_tw" = its tile
  * width (32 / 64). */
 int snrse_get_option(const char* name, int* value);

@@ -1872,7 +1872,12 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
         cx.last_ksplit = 1;
         return launch_x3h(q, stream, x3h_tiles, cx.x3_spread);
       }
-      if (q.gn_scale) return SNRSE_EINVAL;  // the fused GroupNorm exists on the halo form only
+      if (q.Cout <= 16 && cx.conv_variant != 1 && head_ok(q)) {  // the pyramid heads, GroupNorm fused
+        cx.last_kernel = 11;
+        cx.last_ksplit = 1;
+        return launch_head_x3(q, stream);
+      }
+      if (q.gn_scale) return SNRSE_EINVAL;  // the fused GroupNorm exists on the halo forms only
       cx.last_kernel = 3;
       if (q.Cout <= 16) return launch_x3<128, 16, 4, 1>(q, stream, cx);  // the pyramid heads (16 padded rows)
       if (cx.x3_tile == 2) return launch_x3<256, 128, 4, 2>(q, stream, cx);

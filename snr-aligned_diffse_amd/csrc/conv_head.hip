@@ -144,6 +144,154 @@ __global__ __launch_bounds__(256) void conv_head_kernel(ConvParams p) {
 }
 #undef KH_LOAD
 
+// fp32 form for the split-bf16 parity mode (SNRSE_F32X3): fp32 activations, weights pre-split per 32-element
+// K-tile into 32 hi then 32 lo bf16 (ops.split_weight).  Each halo vector (8 fp32 channels, 2 x 16 B) gets
+// the GroupNorm(+SiLU) in fp32 exactly as conv_x3h_kernel applies it, then is split into hi = bf16(x) and
+// lo = bf16(x - hi) halves stored in two LDS halos; every tap accumulates hi.hi + hi.lo + lo.hi.  Replaces
+// the fp32 mode's separate gn_act pass and register-staged Cout <= 16 GEMM (the fp32 input is read once).
+constexpr int KH3_WP = 2 * KH_WP;                // hi + lo weight pieces of one chunk
+constexpr int KH3_WJ = (KH3_WP + 255) / 256;     // per thread (5)
+constexpr int KH3_LDS = 2 * KH_HALO + 2 * 9 * 1024;  // 61,952 B
+
+#define KH3_LOAD(C_)                                                                                           \
+  do {                                                                                                         \
+    const int ch_ = (C_) * 32;                                                                                 \
+    const bool u1_ = ch_ >= p.C0;                                                                              \
+    const __amdgpu_buffer_rsrc_t r_ = u1_ ? make_rsrc(p.src1, p.bytes1) : make_rsrc(p.src0, p.bytes0);         \
+    const int cs_ = u1_ ? p.C1 : p.C0, cc_ = (u1_ ? ch_ - p.C0 : ch_) + hcol * 8;                              \
+    _Pragma("unroll") for (int j = 0; j < KH_HJ; ++j) {                                                        \
+      const int voff_ = hok[j] ? (hpix[j] * cs_ + cc_) * 4 : (int)0x80000000;                                  \
+      hv0[j] = __builtin_amdgcn_raw_buffer_load_b128(r_, voff_, 0, 0);                                         \
+      hv1[j] = __builtin_amdgcn_raw_buffer_load_b128(r_, voff_ + 16, 0, 0);                                    \
+    }                                                                                                          \
+    _Pragma("unroll") for (int k = 0; k < KH3_WJ; ++k) {                                                       \
+      const int pc_ = tid + 256 * k, h_ = pc_ >= KH_WP, pp_ = pc_ - h_ * KH_WP;                                \
+      /* tap (pp >> 6), co ((pp >> 2) & 15), 16-B chunk (pp & 3) of the hi (h = 0) or lo (h = 1) half */       \
+      const int voff_ = pc_ < KH3_WP ? ((((pp_ >> 2) & 15) * 2 * K1 + 2 * ((pp_ >> 6) * Cin + ch_) + h_ * 32 +    \
+                                         (pp_ & 3) * 8) * 2)                                                   \
+                                      : (int)0x80000000;                                                       \
+      wv[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, voff_, 0, 0);                                          \
+    }                                                                                                          \
+    if (gn) {                                                                                                  \
+      const float* sp_ = p.gn_scale + (size_t)b * Cin + ch_ + hcol * 8;                                        \
+      const float* hp_ = p.gn_shift + (size_t)b * Cin + ch_ + hcol * 8;                                        \
+      gs0 = *(const f32x4*)sp_;                                                                                \
+      gs1 = *(const f32x4*)(sp_ + 4);                                                                          \
+      gh0 = *(const f32x4*)hp_;                                                                                \
+      gh1 = *(const f32x4*)(hp_ + 4);                                                                          \
+    }                                                                                                          \
+  } while (0)
+
+template <int GNM>
+__global__ __launch_bounds__(256) void conv_head_x3_kernel(ConvParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[KH3_LDS];
+  char* const halo_hi = smem;
+  char* const halo_lo = smem + KH_HALO;
+  char* const wsl_hi = smem + 2 * KH_HALO;
+  char* const wsl_lo = wsl_hi + 9 * 1024;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntw = p.W / KH_TW, nth = p.H / KH_TH;
+  int t = blockIdx.x;
+  const int w0 = (t % ntw) * KH_TW;
+  t /= ntw;
+  const int h0 = (t % nth) * KH_TH;
+  const int b = t / nth;
+  const int Cin = p.C0 + p.C1;
+  const int nc = Cin >> 5;
+  const int K1 = 9 * Cin;
+  const int hcol = tid & 3;
+  constexpr bool gn = GNM > 0;
+  const int lrow = lane & 15, lg = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.wgt, p.wbytes);
+
+  int hpix[KH_HJ];
+  bool hok[KH_HJ];
+#pragma unroll
+  for (int j = 0; j < KH_HJ; ++j) {
+    const int hr = (tid >> 2) + 64 * j;
+    const int hy = hr / KH_HC, hx = hr - hy * KH_HC;
+    const int ih = h0 + hy - 1, iw = w0 + hx - 1;
+    hok[j] = hr < KH_HROWS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+    hpix[j] = (b * p.H + ih) * p.W + iw;
+  }
+  u32x4 hv0[KH_HJ], hv1[KH_HJ], wv[KH3_WJ];
+  f32x4 gs0 = {1.f, 1.f, 1.f, 1.f}, gs1 = gs0, gh0 = {0.f, 0.f, 0.f, 0.f}, gh1 = gh0;
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  KH3_LOAD(0);
+  for (int c = 0; c < nc; ++c) {
+#pragma unroll
+    for (int j = 0; j < KH_HJ; ++j) {
+      const int hr = (tid >> 2) + 64 * j;
+      if (j == KH_HJ - 1 && hr >= KH_HROWS) break;
+      float x[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        x[k] = __uint_as_float(hv0[j][k]);
+        x[4 + k] = __uint_as_float(hv1[j][k]);
+      }
+      if constexpr (gn) {
+        const float sc[8] = {gs0[0], gs0[1], gs0[2], gs0[3], gs1[0], gs1[1], gs1[2], gs1[3]};
+        const float sh[8] = {gh0[0], gh0[1], gh0[2], gh0[3], gh1[0], gh1[1], gh1[2], gh1[3]};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float y = fmaf(x[k], sc[k], sh[k]);
+          x[k] = hok[j] ? (GNM == 2 ? silu(y) : y) : 0.f;  // outside the image: the conv's zero padding
+        }
+      }
+      u32x4 hi, lo;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        hi[k] = pack_bf16x2(x[2 * k], x[2 * k + 1]);
+        lo[k] = pack_bf16x2(x[2 * k] - __uint_as_float(hi[k] << 16), x[2 * k + 1] - __uint_as_float(hi[k] & 0xffff0000u));
+      }
+      *(u32x4*)(halo_hi + kh_swz(hr, hcol)) = hi;
+      *(u32x4*)(halo_lo + kh_swz(hr, hcol)) = lo;
+    }
+#pragma unroll
+    for (int k = 0; k < KH3_WJ; ++k) {
+      const int pc = tid + 256 * k, h = pc >= KH_WP, pp = pc - h * KH_WP;
+      if (pc < KH3_WP) *(u32x4*)((h ? wsl_lo : wsl_hi) + (pp >> 6) * 1024 + kh_swz((pp >> 2) & 15, pp & 3)) = wv[k];
+    }
+    __syncthreads();
+    if (c + 1 < nc) KH3_LOAD(c + 1);
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) {
+      const int dy = tp / 3 - 1, dx = tp % 3 - 1;
+      const int hbase = (wid * KH_RW + dy + 1) * KH_HC + dx + 1 + lrow;
+      const u32x4 ah = *(const u32x4*)(wsl_hi + tp * 1024 + kh_swz(lrow, lg));
+      const u32x4 al = *(const u32x4*)(wsl_lo + tp * 1024 + kh_swz(lrow, lg));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ho = kh_swz(hbase + (16 * i / KH_TW) * KH_HC + (16 * i) % KH_TW, lg);
+        const u32x4 bh = *(const u32x4*)(halo_hi + ho);
+        const u32x4 bl = *(const u32x4*)(halo_lo + ho);
+        acc[i] = mfma_chunk<bf16_t>(ah, bh, acc[i]);
+        acc[i] = mfma_chunk<bf16_t>(ah, bl, acc[i]);
+        acc[i] = mfma_chunk<bf16_t>(al, bh, acc[i]);
+      }
+    }
+    __syncthreads();
+  }
+  const int co = 4 * lg;
+  if (co < p.Cout) {
+    f32x4 add = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias) add = f32x4{p.bias[co], p.bias[co + 1], p.bias[co + 2], p.bias[co + 3]};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const size_t m = ((size_t)b * p.H + h0 + wid * KH_RW + 16 * i / KH_TW) * p.W + w0 + (16 * i) % KH_TW + lrow;
+      f32x4 v = acc[i] + add;
+      if (p.res) v += *(const f32x4*)((const float*)p.res + m * p.res_ld + co);
+      v *= p.out_scale;
+      *(f32x4*)((float*)p.out + m * p.out_ld + co) = v;
+    }
+  }
+}
+#undef KH3_LOAD
+
 }  // namespace
 
 bool head_ok(const ConvParams& p) {
@@ -162,6 +310,17 @@ int launch_head(const ConvParams& p, hipStream_t s) {
   if (!p.gn_scale) hipLaunchKernelGGL(conv_head_kernel<0>, dim3((unsigned)tiles), dim3(256), 0, s, p);
   else if (!p.gn_act) hipLaunchKernelGGL(conv_head_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, s, p);
   else hipLaunchKernelGGL(conv_head_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  return (int)hipGetLastError();
+}
+
+// the split-bf16 form: same shape contract, fp32 activations (p.bytes* are fp32 extents)
+int launch_head_x3(const ConvParams& p, hipStream_t s) {
+  if (!head_ok(p)) return SNRSE_EINVAL;
+  const long long tiles = (long long)p.B * (p.H / KH_TH) * (p.W / KH_TW);
+  if (tiles <= 0 || tiles > 0x7fffffffLL) return SNRSE_EINVAL;
+  if (!p.gn_scale) hipLaunchKernelGGL(conv_head_x3_kernel<0>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  else if (!p.gn_act) hipLaunchKernelGGL(conv_head_x3_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(conv_head_x3_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, s, p);
   return (int)hipGetLastError();
 }
 

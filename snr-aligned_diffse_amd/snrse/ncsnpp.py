@@ -184,14 +184,17 @@ class NCSNppHIP:
         W["dense_b"] = torch.cat(dense_b, 0).contiguous()
         if gemm == "x3":
             W["in_w"] = ops.split_weight(W["in_w"])
-            # (the pyramid heads stay exact: split, they measured no faster within box variance and moved
-            # the PC golden's error from 5.7e-5 to 6.7e-5 absolute, profiles/r03zG)
+            # the pyramid heads split too: their fused-GroupNorm halo kernel (conv_head_x3_kernel) reads the
+            # fp32 input once instead of a gn_act pass + the register-staged Cout <= 16 GEMM (split heads on
+            # the register-staged GEMM alone measured no faster, profiles/r03zG)
             for m in self.plan:
                 e = self.mw[m.idx]
                 if m.kind == "rb":
                     for k in ("w0", "w1", "w2"):
                         if k in e:
                             e[k] = ops.split_weight(e[k])
+                elif m.kind == "conv3x3" and "w" in e:
+                    e["w"] = ops.split_weight(e["w"])
 
     # ------------------------------------------------------------------ blocks
     # Every activation travels with its per-channel GroupNorm statistics, produced by the
@@ -253,7 +256,7 @@ class NCSNppHIP:
         g = self.mw[gn_m.idx]
         c = self.mw[conv_m.idx]
         t, s = h
-        if ops.head_ok(t):  # GroupNorm+SiLU fused into the head conv's halo load
+        if ops.head_ok(t, split=self.gemm == "x3"):  # GroupNorm+SiLU fused into the head conv's halo load
             gn = ops.gn_scale_shift(s, g["g"], g["b"], t.shape[1] * t.shape[2])
             return ops.conv2d(t, c["w"], 3, 4, bias=c["b"], res=pyr_up, out_f32=True, gn=gn)
         a = ops.gn_apply(t, None, s, g["g"], g["b"], act=True)

@@ -231,7 +231,7 @@ def probe_read(max_calls, dev=None, all_threads=False):
 
 KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 3: "conv_x3_kernel", 4: "conv_x3h_kernel",
            5: "conv_halo5_kernel",
-           10: "conv_head_kernel"}
+           10: "conv_head_kernel", 11: "conv_head_x3_kernel"}
 
 
 def kernel_name(gen):
@@ -266,12 +266,13 @@ def x3h_ok(x, ksize, cout):
     return t == 4 or (t == 0 and B * (H // 4) * (-(-W // 64)) * (cout // 128) >= 256)
 
 
-def head_ok(x):
-    """True when a bf16 3x3 conv of x with Cout <= 16 and f32 output (the pyramid heads) takes the
-    halo-staged head kernel, which accepts a fused GroupNorm (gn=)."""
+def head_ok(x, split=False):
+    """True when a 3x3 conv of x with Cout <= 16 and f32 output (the pyramid heads) takes the halo-staged
+    head kernel, which accepts a fused GroupNorm (gn=): bf16 x, or f32 x with split weights (split=True,
+    the fp32x3 mode's conv_head_x3_kernel)."""
     B, H, W, C = x.shape
-    return (x.dtype == torch.bfloat16 and H % 8 == 0 and W % 32 == 0 and C % 32 == 0
-            and _opt(x, "conv_variant") != 1)
+    dt_ok = x.dtype == torch.bfloat16 or (split and x.dtype == torch.float32)
+    return dt_ok and H % 8 == 0 and W % 32 == 0 and C % 32 == 0 and _opt(x, "conv_variant") != 1
 
 
 def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):

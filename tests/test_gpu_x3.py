@@ -121,6 +121,38 @@ def test_x3_pyramid_head(gpu):
     assert rel(nchw(out), ref) < TOL
 
 
+@pytest.mark.parametrize("gnm", [0, 1, 2])
+@pytest.mark.parametrize("shape", [(2, 128, 8, 32), (1, 256, 16, 64), (2, 128, 24, 96), (1, 64, 8, 32)])
+def test_x3_pyramid_head_fused(gpu, shape, gnm):
+    """The split-bf16 halo head (conv_head_x3_kernel, H % 8 == 0, W % 32 == 0): conv3x3(act(GN(x)), C -> 4)
+    + bias + the upsampled pyramid residual, gnm 0 raw x, 1 GroupNorm, 2 GroupNorm+SiLU (ncsnpp.py:348-366)."""
+    from snrse import ops
+    B, cin, H, W = shape
+    x = torch.from_numpy(fnormal("t.pyf.x", (B, cin, H, W))) * 1.5 + 0.2
+    w = torch.from_numpy(fnormal("t.pyf.w", (4, cin, 3, 3))) / math.sqrt(9 * cin)
+    b = torch.from_numpy(fnormal("t.pyf.b", (4,)))
+    r = torch.from_numpy(fnormal("t.pyf.r", (B, 4, H, W)))
+    g = torch.from_numpy(fnormal("t.pyf.g", (cin,))) * 0.1 + 1
+    be = torch.from_numpy(fnormal("t.pyf.be", (cin,))) * 0.1
+    a = x.double()
+    if gnm:
+        a = F.group_norm(a, min(cin // 4, 32), g.double(), be.double(), eps=1e-6)
+        a = F.silu(a) if gnm == 2 else a
+    ref = F.conv2d(a, w.double(), b.double(), padding=1) + r.double()
+    xg = nhwc(x).to(gpu)
+    gn = None
+    if gnm:
+        sums, _ = ops.gn_stats(xg)
+        gn = ops.gn_scale_shift(sums, g.to(gpu), be.to(gpu), H * W)
+    wp = torch.cat([w.permute(0, 2, 3, 1).reshape(4, -1), torch.zeros(12, 9 * cin)]).to(gpu)
+    assert ops.head_ok(xg, split=True) and not ops.head_ok(xg)
+    out = ops.conv2d(xg, ops.split_weight(wp), 3, 4, bias=b.to(gpu), res=nhwc(r).to(gpu), out_f32=True, gn=gn,
+                     gn_act=gnm == 2)
+    assert ops.get_option("last_kernel") == 11
+    assert out.dtype == torch.float32
+    assert rel(nchw(out), ref) < TOL
+
+
 def test_x3_level0_vs_exact_fp32(gpu):
     """One C2 level-0 shape (256 x 512, 128 -> 128) on two images: the split halo kernel vs the exact-fp32
     kernel."""
