@@ -1350,9 +1350,6 @@ __global__ __launch_bounds__(256) void conv_splitk_finalize(ConvParams p, int pp
 #ifndef SNRSE_H5_OPAQUE
 #define SNRSE_H5_OPAQUE 0
 #endif
-#ifndef SNRSE_H5_DRAIN
-#define SNRSE_H5_DRAIN 0
-#endif
 SNRSE_DEV int h5_opaque(int v) {
   int r;
   asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
@@ -1578,20 +1575,6 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   epilogue_img<TO, 4, 128, true, EF, TW>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0, p.W - TW);
   SNRSE_STAMP(27);
   if (EF < 0 ? p.stats != nullptr : (EF & EF_STATS) != 0) block_stats_flush<4, 128>(p, red, bb, n0);
-#if SNRSE_H5_DRAIN
-  // cost probe of a producer-side GroupNorm fold (A/B build only): every wave drains its
-  // stores and statistics atomics, then one lane takes an arrival ticket (a returning agent-scope atomic
-  // add of 0 to the block's first statistics word, so the data is unchanged) that the block waits for
-  if (p.stats) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (tid == 0) {
-      const double t = atomicAdd(&p.stats[stat_idx(bb, blockIdx.x & (SNRSE_STAT_SLOTS - 1), n0, p.Cout)], 0.0);
-      gnl[0] = (float)t;
-    }
-    __builtin_amdgcn_s_barrier();
-  }
-#endif
 #ifdef SNRSE_STAMPS
   {
     unsigned long long st_[29];
