@@ -49,3 +49,15 @@ def test_split_weight_layout():
     hi, lo = t[:, :, 0].reshape(3, 96), t[:, :, 1].reshape(3, 96)
     assert torch.equal(hi, w.to(torch.bfloat16).float())
     assert ((hi + lo - w).abs() <= w.abs() * 2.0 ** -16).all()
+
+
+def test_resample_shape_contract():
+    """ops.resample_ok mirrors snrse_gn_resample's contract: bf16 C % 16 == 0 (row strips / LDS tiles), f32
+    C % 4 == 0 with C / 4 dividing 64 (row strips only); other dtypes go through snrse_gn_apply."""
+    import torch
+    from snrse import ops
+    ok = lambda c, dt: ops.resample_ok(torch.empty(1, 2, 2, c, dtype=dt))  # noqa: E731
+    assert ok(128, torch.bfloat16) and ok(256, torch.bfloat16) and not ok(8, torch.bfloat16)
+    assert ok(4, torch.float32) and ok(128, torch.float32) and ok(256, torch.float32)
+    assert not ok(512, torch.float32) and not ok(12, torch.float32) and not ok(6, torch.float32)
+    assert not ok(128, torch.float16)
