@@ -153,6 +153,28 @@ def test_x3_pyramid_head_fused(gpu, shape, gnm):
     assert rel(nchw(out), ref) < TOL
 
 
+def test_x3_pyramid_head_level0_vs_exact_fp32(gpu):
+    """The level-0 pyramid head at C2 size on two images (256 x 512, 128 -> 4, GroupNorm+SiLU fused, upsampled
+    pyramid residual): the split halo head vs the exact-fp32 path (gn_apply pass + register-staged fp32 GEMM)."""
+    from snrse import ops
+    B, C, H, W = 2, 128, 256, 512
+    g = torch.Generator(device=gpu).manual_seed(5)
+    x = torch.randn(B, H, W, C, device=gpu, generator=g) * 1.5 + 0.2
+    w = torch.cat([torch.randn(4, 9 * C, device=gpu, generator=g) / math.sqrt(9 * C),
+                   torch.zeros(12, 9 * C, device=gpu)])
+    b = torch.randn(4, device=gpu, generator=g)
+    r = torch.randn(B, H, W, 4, device=gpu, generator=g)
+    gam = torch.rand(C, device=gpu, generator=g) + 0.5
+    bet = torch.randn(C, device=gpu, generator=g) * 0.1
+    sums, _ = ops.gn_stats(x)
+    exact = ops.conv2d(ops.gn_apply(x, None, sums, gam, bet, act=True), w, 3, 4, bias=b, res=r, out_f32=True)
+    assert ops.get_option("last_kernel") == 1
+    gn = ops.gn_scale_shift(sums, gam, bet, H * W)
+    split = ops.conv2d(x, ops.split_weight(w), 3, 4, bias=b, res=r, out_f32=True, gn=gn)
+    assert ops.get_option("last_kernel") == 11
+    assert rel(split, exact) < TOL
+
+
 def test_x3_level0_vs_exact_fp32(gpu):
     """One C2 level-0 shape (256 x 512, 128 -> 128) on two images: the split halo kernel vs the exact-fp32
     kernel."""
