@@ -551,12 +551,19 @@ def run(args):
         if args.dtype == "fp32x3":  # the golden's [2, 256, 64] grid is small: force the benched halo kernel
             ops.set_option("x3_tile", 4)  # (conv_x3h_kernel + fused GroupNorm) wherever its shape allows
         try:
-            r = paritycheck.pc_vs_golden(dev, net)
+            if args.config == "c4":  # the timed SNR-aligned path on the reference's C4 run
+                r = paritycheck.c4_vs_golden(dev, net)
+            else:
+                r = paritycheck.pc_vs_golden(dev, net)
         finally:
             ops.set_option("x3_tile", 0)
-        parity = {k: r[k] for k in ("check", "dtype", "rel_rms", "abs_rms", "golden_rms", "tol_rel", "ok")}
-        parity["golden"] = "tests/golden/pc_ouve.npz"
-        if r["dtype"] in ("fp32", "fp32x3"):  # the north star's bound: 1e-4 absolute RMS on the complex spectrogram
+        if args.config == "c4":
+            parity = {k: r[k] for k in ("check", "dtype", "rel_rms", "t_hat_abs_err", "tol_rel", "ok")}
+            parity["golden"] = "tests/golden/enhance_snrnet_c4.npz"
+        else:
+            parity = {k: r[k] for k in ("check", "dtype", "rel_rms", "abs_rms", "golden_rms", "tol_rel", "ok")}
+            parity["golden"] = "tests/golden/pc_ouve.npz"
+        if r["dtype"] in ("fp32", "fp32x3") and "abs_rms" in r:  # the north star's 1e-4 absolute RMS bound
             parity["tol_abs"] = 1e-4
             parity["ok"] = bool(parity["ok"] and r["abs_rms"] < 1e-4)
 

@@ -11,6 +11,9 @@ tolerance it is held to, so a driver-run record (smoke log, bench JSON line) car
   (conv_halo5_kernel: B=32, 256 x 512, 128 -> 128, GroupNorm+SiLU prologue, temb, statistics,
   non-temporal epilogue) against fp32 F.conv2d of the same bf16 operands on three images
   (reference layerspp.py:244-266).
+* `c4_vs_golden`: the C4 path exactly as `bench.py --config c4` times it (snrse.enhance.SNRAlignedEnhancer:
+  SNRNet estimate -> t_hat -> one preconditioned sebridge_v3 NFE) on the reference's own C4 run
+  (tests/golden/enhance_snrnet_c4.npz; model.py:702-839, snrnet.py:47-97) with its noise draws.
 * `pc_vs_golden`: the PC loop exactly as bench.py times it (snrse.enhance.PCEnhancer on the given net)
   for the reference's own N = 5 OUVE run (tests/golden/pc_ouve.npz; sampling/__init__.py:54-75,
   predictors.py:75-80, correctors.py:69-81) with the recorded noise draws.
@@ -37,7 +40,10 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 # BF16_PC_TOL); the fp32 parity mode to 1e-4 (the north star's bound).  One halo launch vs fp32 conv of
 # the same bf16 operands: 1e-2 (test_halo_c2_level0_nontemporal).
 TOL = {"nfe": {"bf16": 2e-2, "fp32": 1e-4, "fp32x3": 1e-4}, "pc": {"bf16": 2e-2, "fp32": 1e-4, "fp32x3": 1e-4},
-       "halo": 1e-2}
+       "halo": 1e-2, "c4": {"bf16": 3e-2, "fp32": 1e-4, "fp32x3": 1e-4}}
+# C4 bf16: x_hat is one bf16 network evaluation scaled by c_out (+ c_skip x_t) on real VBD clips; measured
+# 2.1e-2 relative (profiles/r03zX_c4_bench_line.json) against 1.5e-2 for one NFE on the synthetic
+# ncsnpp_full input, so the one-step check is held to 3e-2 (the fp32 path: 1e-4, test_gpu_c2_path.py).
 
 
 def _golden(name):
@@ -141,4 +147,37 @@ def pc_vs_golden(dev, net=None, dtype=torch.bfloat16):
          "dtype": d, "nfe": nfe, "rel_rms": _rel(x, g["out"][:, 0]), "abs_rms": _abs_rms(x, g["out"][:, 0]),
          "golden_rms": float(np.sqrt(np.mean(np.abs(g["out"]) ** 2))), "tol_rel": TOL["pc"][d]}
     r["ok"] = bool(nfe == 10 and np.isfinite(r["rel_rms"]) and r["rel_rms"] < r["tol_rel"])
+    return r
+
+
+def c4_vs_golden(dev, net):
+    """SNRAlignedEnhancer (bench.py --config c4's class) on the reference's C4 run: the golden's noisy
+    int16 clips, its SNRNet weights (formula weights with the fc bias shifted by -2.1, tools/gen_golden.py
+    C4_FC_BIAS_SHIFT) and noise draws; t_hat exact (fp32 SNRNet), x_hat to the net's tolerance."""
+    from sgmse.backbones import SNRNet
+    from snrse import formula
+    from snrse.enhance import SNRAlignedEnhancer, pad_frames
+    g = _golden("enhance_snrnet_c4.npz")
+    with open(os.path.join(GOLDEN, "state_dict_keys.json")) as f:
+        shapes = {"snrnet." + k: tuple(sh) for k, sh in json.load(f)["snrnet"]}
+    sd = {k[len("snrnet."):]: torch.from_numpy(v) for k, v in formula.formula_state_dict(shapes).items()}
+    sd["fc.bias"] = sd["fc.bias"] - 2.1
+    snr = SNRNet()
+    snr.load_state_dict(sd)
+    ys = g["noisy_i16"].astype(np.float32) / 32768.0
+    B, L = ys.shape
+    Tp = pad_frames(1 + L // 128)
+    Z = torch.stack([torch.from_numpy(formula.normal_tensor(f"golden.c4.Z.{k}", (1, 1, 256, Tp), True))[0, 0]
+                     for k in range(B)]).to(dev).contiguous()
+    enh = SNRAlignedEnhancer(net, snr_fn=lambda spec: (lambda gt: gt / (1 - gt))(snr.forward_complex(spec)[:, 0]),
+                             fixed_snr=0.17783, sigma_max=0.5)
+    xh, t_hat = enh(torch.from_numpy(ys).to(dev), noise=Z)
+    torch.cuda.synchronize(dev)
+    d = _dtname(net)
+    errs = [_rel(xh[k], g["x_hat"][k]) for k in range(B)]
+    r = {"check": f"SNRAlignedEnhancer (SNRNet t_hat + one sebridge_v3 NFE) on {B} reference clips vs golden "
+                  "enhance_snrnet_c4.npz", "dtype": d, "rel_rms": max(errs),
+         "t_hat_abs_err": float(np.max(np.abs(np.asarray(t_hat, dtype=np.float64) - g["t_hat"]))),
+         "tol_rel": TOL["c4"][d]}
+    r["ok"] = bool(np.isfinite(r["rel_rms"]) and r["rel_rms"] < r["tol_rel"] and r["t_hat_abs_err"] < 1e-12)
     return r
