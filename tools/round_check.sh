@@ -7,4 +7,5 @@ bash tools/gpu_step.sh $OUT \
   "tests:::900:::python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
   "smoke:::200:::python -u -c 'import __graft_entry__ as g; g.smoke()'" \
   "bench:::300:::python -u bench.py" \
+  "c4:::300:::python -u bench.py --config c4" \
   "x3prof:::900:::bash tools/prof_x3.sh ${TAG}_x3 fp32x3"
