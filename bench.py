@@ -342,6 +342,7 @@ class ConvProbe:
 
     def __init__(self, all_threads=False):
         self.rec = []
+        self.chunks = []
         self.all_threads = all_threads  # also the other threads' contexts (the autograd worker's backward)
 
     def install(self, ops):
@@ -351,7 +352,10 @@ class ConvProbe:
         def wrapped(src0, wgt, ksize, cout, *a, **kw):
             big = ops.halo_ok(src0, ksize, cout) or (src0.dtype == torch.float32 and ksize == 3 and cout >= 64)
             probe.rec.append(conv_flops(src0, kw.get("src1"), ksize, cout, kw.get("sc"), kw.get("sc1")) if big else None)
-            return orig(src0, wgt, ksize, cout, *a, **kw)
+            out = orig(src0, wgt, ksize, cout, *a, **kw)
+            # launches of this call: sources beyond 2 GiB (fp32 level 0 at B = 32) run as image-range chunks
+            probe.chunks.append(max(1, ops._opt(src0, "last_chunks")) if big else 1)
+            return out
 
         ops.conv2d = wrapped
         self.orig, self.ops = orig, ops
@@ -361,7 +365,8 @@ class ConvProbe:
         self.ops.conv2d = self.orig
 
     def summary(self):
-        """{kernel: [flops, ms, launches]} over the probed pass."""
+        """{kernel: [flops, ms, launches]} over the probed pass (launches: kernel launches, counting each
+        image-range chunk of a call whose sources exceed 2 GiB)."""
         ms, kern = self.ops.probe_read(self.CAP, all_threads=self.all_threads)
         self.ops.probe_begin(0, all_threads=self.all_threads)
         if len(ms) != min(len(self.rec), self.CAP):
@@ -370,13 +375,13 @@ class ConvProbe:
             with open(os.environ["SNRSE_PROBE_DUMP"], "w") as f:
                 json.dump({"ms": ms, "kernel": kern, "flops": self.rec[:len(ms)]}, f)
         by = {}
-        for fl, t, k in zip(self.rec, ms, kern):
+        for fl, t, k, nl in zip(self.rec, ms, kern, self.chunks):
             if fl is None:
                 continue
             d = by.setdefault(self.ops.kernel_name(k), [0.0, 0.0, 0])
             d[0] += fl
             d[1] += t
-            d[2] += 1
+            d[2] += nl
         return by
 
 
