@@ -373,7 +373,7 @@ class ConvProbe:
             raise RuntimeError(f"probe: {len(ms)} timed calls for {len(self.rec)} conv2d calls")
         if os.environ.get("SNRSE_PROBE_DUMP"):  # per-call record for tools/probe_reconcile.py
             with open(os.environ["SNRSE_PROBE_DUMP"], "w") as f:
-                json.dump({"ms": ms, "kernel": kern, "flops": self.rec[:len(ms)]}, f)
+                json.dump({"ms": ms, "kernel": kern, "flops": self.rec[:len(ms)], "launches": self.chunks[:len(ms)]}, f)
         by = {}
         for fl, t, k, nl in zip(self.rec, ms, kern, self.chunks):
             if fl is None:
