@@ -573,8 +573,10 @@ def run(args):
             parity["ok"] = bool(parity["ok"] and r["abs_rms"] < 1e-4)
 
     # The same C2 workload in the fp32x3 parity mode (split-bf16 fp32 GEMMs: within the north star's 1e-4
-    # RMS) beside the bf16 headline, single-GPU default runs only: one warm-up and one timed step, then its
-    # own N=5 PC golden check (halo kernel forced at the golden's size)
+    # RMS) beside the bf16 headline, single-GPU default runs only: one warm-up step, then K3 = max(3, --steps)
+    # timed steps on the timed run's clips and noise seeds, the dominant x3 kernel's probe fraction, its own
+    # N=5 PC golden check (halo kernel forced at the golden's size) and the C2-size agreement of the timed
+    # bf16 output with the x3 output of the same clips and Philox seed (c2_agreement)
     pmode = None
     if (world == 1 and args.config == "c2" and args.dtype == "bf16" and not args.no_parity_mode
             and args.seconds == 4.0 and args.N == 30):
@@ -582,24 +584,53 @@ def run(args):
         torch.cuda.empty_cache()
         net3 = ncsnpp.NCSNppHIP(formula_weights(), dtype=torch.float32, device=dev, gemm="x3")
         enh3 = PCEnhancer(net3, sde, N=args.N)
+        K3 = max(3, args.steps)
         enh3(y, noise(50))
         torch.cuda.synchronize()
         t3 = time.perf_counter()
-        enh3(y, noise(150))
+        for k in range(K3):
+            xh3, _ = enh3(y, noise(100 + k))  # the bf16 timed steps' seeds
         torch.cuda.synchronize()
         el3 = time.perf_counter() - t3
-        pmode = {"dtype": "fp32x3", "value": B / el3, "unit": "utt/s", "ms_per_step": el3 * 1e3, "steps": 1,
-                 "warmup": 1, "note": ("fp32 activations / storage / accumulation, ResBlock and input convs as "
-                                       "split-bf16 GEMMs (bench.py --dtype fp32x3 for the full line)")}
+        pmode = {"dtype": "fp32x3", "value": K3 * B / el3, "unit": "utt/s", "ms_per_step": el3 / K3 * 1e3,
+                 "steps": K3, "warmup": 1,
+                 "note": ("fp32 activations / storage / accumulation, ResBlock and input convs as "
+                          "split-bf16 GEMMs (bench.py --dtype fp32x3 for the full line)")}
+        # the x3 output for the bf16 timed run's last seed (100 + steps - 1): the K3-th timed step when
+        # K3 == steps, else one more untimed step
+        if K3 != args.steps:
+            xh3, _ = enh3(y, noise(100 + args.steps - 1))
+        import paritycheck
+        pmode["c2_agreement"] = paritycheck.waveform_agreement(xh, xh3)
+        pmode["c2_agreement"]["what"] = (f"timed bf16 C2 output vs fp32x3 on the same {B} clips and Philox seed "
+                                         f"(N={args.N}, {nfe} NFE/utt)")
+        if not args.no_probe:
+            probe = ConvProbe()
+            probe.install(ops)
+            try:
+                PCEnhancer(net3, sde, N=2)(y, noise(999))
+            finally:
+                probe.uninstall()
+            by = probe.summary()
+            kn = max(by, key=lambda k: by[k][1])
+            fl, ms, n = by[kn]
+            pmode["roofline"] = {"kernel": kn, "bound": "mfma", "achieved": fl / (ms * 1e-3) / 1e12,
+                                 "peak": PEAK["fp32x3"] / 1e12, "unit": "TFLOP/s (fp32-equivalent)",
+                                 "frac": fl / (ms * 1e-3) / PEAK["fp32x3"], "launches_per_pass": n,
+                                 "avg_launch_us": ms * 1e3 / max(n, 1)}
         if not args.no_parity:
-            import paritycheck
             ops.set_option("x3_tile", 4)
             try:
                 r3 = paritycheck.pc_vs_golden(dev, net3)
             finally:
                 ops.set_option("x3_tile", 0)
             pmode["parity"] = {"abs_rms": r3["abs_rms"], "rel_rms": r3["rel_rms"], "tol_abs": 1e-4,
-                               "ok": bool(r3["ok"] and r3["abs_rms"] < 1e-4), "golden": "tests/golden/pc_ouve.npz"}
+                               "ok": bool(r3["ok"] and r3["abs_rms"] < 1e-4), "golden": "tests/golden/pc_ouve.npz",
+                               "kernels": "x3_tile=4: conv_x3h_kernel forced wherever its shape allows"}
+            r30 = paritycheck.pc_vs_golden(dev, net3)  # the dispatch the timed steps ran (x3_tile 0)
+            pmode["parity"]["timed_dispatch"] = {"abs_rms": r30["abs_rms"], "rel_rms": r30["rel_rms"],
+                                                 "ok": bool(r30["ok"] and r30["abs_rms"] < 1e-4)}
+            pmode["parity"]["ok"] = bool(pmode["parity"]["ok"] and pmode["parity"]["timed_dispatch"]["ok"])
         del enh3, net3
         torch.cuda.empty_cache()
 

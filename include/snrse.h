@@ -37,6 +37,9 @@ typedef struct ihipStream_t* hipStream_t;
 enum { SNRSE_F32 = 0, SNRSE_BF16 = 1, SNRSE_F16 = 2, SNRSE_F64 = 3, SNRSE_F32X3 = 4 };
 
 int snrse_abi_version(void); /* 2: snrse_ctx arguments */
+/* sha256 (hex) of the sources the library was compiled from: csrc/*.hip, *.cpp, *.h and the build
+ * script (snrse/build.py source_hash()), compiled in; "unknown" for a build made without it. */
+const char* snrse_build_id(void);
 const char* snrse_error_string(int code);
 int snrse_device_name(char* buf, int len);
 
@@ -124,7 +127,10 @@ int snrse_gn_apply(const void* src0, int C0, const void* src1, int C1, int B, in
  * layerspp.py:249/255), both [B][Ho][Wo][C] from one pass over x.  scale/shift [B][C] f32 from
  * snrse_gn_scale_shift, or both NULL (identity).  mode 1 down (H, W even), 2 up.  dtype SNRSE_BF16: C % 8 == 0
  * with C / 8 dividing 64 (the row-strip kernel), otherwise C % 16 == 0 (the LDS-tiled kernel); SNRSE_F32
- * (the fp32 parity modes): C % 4 == 0 with C / 4 dividing 64 (row strips). */
+ * (the fp32 parity modes): C % 4 == 0 with C / 4 dividing 64 (row strips).  act = 1 computes SiLU in both
+ * dtypes as z * rcp(-(1 + 2^z) / ln 2) on the affine prescaled by -log2(e) (v_exp_f32 + v_rcp_f32, each 1 ulp:
+ * a few fp32 ulp, ~4e-7 relative), not the IEEE-division silu_exact of snrse_gn_act / snrse_gn_apply; in the
+ * exact fp32 mode that is 2-3 orders below its 1e-4 tolerance (tests/test_gpu_kernels.py resample cases). */
 int snrse_gn_resample(snrse_ctx* ctx, const void* src, int C, int B, int H, int W, const float* scale, const float* shift,
                       int act, int mode, void* out_act, void* out_raw, int dtype, hipStream_t stream);
 

@@ -150,6 +150,30 @@ def pc_vs_golden(dev, net=None, dtype=torch.bfloat16):
     return r
 
 
+# C2-size agreement of the benched bf16 output with the fp32x3 parity mode on the same 32 clips and the same
+# Philox draws (N = 30, 60 NFE): bf16 vs exact fp32 at B = 2 measured 32 dB SI-SDR / 2.5e-2 relative RMS
+# (profiles/r02a_c2_bf16_vs_fp32.json); held to >= 25 dB per clip and <= 5e-2 relative RMS per clip.
+C2_AGREE = {"si_sdr_min_db": 25.0, "rel_rms_max": 5e-2}
+
+
+def waveform_agreement(est, ref):
+    """Per-utterance agreement of waveforms est [B, L] with ref [B, L] (float64): SI-SDR of est against ref as
+    the reference computes it (sgmse/util/other.py:71-75: alpha = <est, ref> / |ref|^2, 10 log10 |alpha ref|^2 /
+    |alpha ref - est|^2) and the relative RMS |est - ref| / |ref|; minimum / maximum over the batch."""
+    e = torch.as_tensor(est).detach().to(torch.float64)
+    r = torch.as_tensor(ref).detach().to(torch.float64)
+    alpha = (e * r).sum(1) / r.pow(2).sum(1)
+    tgt = alpha[:, None] * r
+    sisdr = 10 * torch.log10(tgt.pow(2).sum(1) / (tgt - e).pow(2).sum(1))
+    relr = (e - r).pow(2).sum(1).sqrt() / r.pow(2).sum(1).sqrt()
+    out = {"si_sdr_bf16_vs_x3_db_min": float(sisdr.min()), "si_sdr_bf16_vs_x3_db_mean": float(sisdr.mean()),
+           "rel_rms_max": float(relr.max()), "rel_rms_mean": float(relr.mean()), "clips": int(e.shape[0])}
+    out["ok"] = bool(np.isfinite(out["si_sdr_bf16_vs_x3_db_min"]) and out["si_sdr_bf16_vs_x3_db_min"] >= C2_AGREE["si_sdr_min_db"]
+                     and out["rel_rms_max"] <= C2_AGREE["rel_rms_max"])
+    out["bounds"] = dict(C2_AGREE)
+    return out
+
+
 def c4_vs_golden(dev, net):
     """SNRAlignedEnhancer (bench.py --config c4's class) on the reference's C4 run: the golden's noisy
     int16 clips, its SNRNet weights (formula weights with the fc bias shifted by -2.1, tools/gen_golden.py

@@ -8,6 +8,13 @@
 
 extern "C" int snrse_abi_version(void) { return 2; }
 
+// Source hash of the tree this library was compiled from (snrse/build.py: sha256 over csrc/* and the
+// build script, passed as -DSNRSE_BUILD_ID), so a run can show that the binary it loaded matches HEAD.
+#ifndef SNRSE_BUILD_ID
+#define SNRSE_BUILD_ID "unknown"
+#endif
+extern "C" const char* snrse_build_id(void) { return SNRSE_BUILD_ID; }
+
 extern "C" const char* snrse_error_string(int code) { return hipGetErrorString((hipError_t)code); }
 
 // Name and gfx target of the current device into `buf` (nul-terminated); returns 0 or a hipError_t.

@@ -1863,11 +1863,16 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
   p.ntn = 1;
   if (stats && !cx.stats_zeroed) SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * Cout, stream));
   if (dtype != SNRSE_BF16 && dtype != SNRSE_F32) return SNRSE_EINVAL;
+  // the split-bf16 halo-kernel decision is taken once for the whole batch (as ops.x3h_ok takes it, which
+  // decides whether the caller passes a GroupNorm prologue), so every image-range chunk of a > 2 GiB call
+  // runs the same kernel, however few tiles its last chunk has
+  const bool x3h_all = x3 && ksize == 3 && H % x3h::TH == 0 && Cout % 128 == 0 &&
+                       ((cx.x3_tile == 0 && (long long)B * (H / x3h::TH) * ((W + x3h::TW - 1) / x3h::TW) * (Cout / 128) >= 256) ||
+                        cx.x3_tile == 4);
   auto run = [&](const ConvParams& q) {
     if (x3) {
       const int x3h_tiles = q.B * (q.H / x3h::TH) * ((q.W + x3h::TW - 1) / x3h::TW) * (q.Cout / 128);
-      const bool x3h_ok = q.ksize == 3 && q.H % x3h::TH == 0 && q.Cout % 128 == 0;
-      if (x3h_ok && ((cx.x3_tile == 0 && x3h_tiles >= 256) || cx.x3_tile == 4)) {
+      if (x3h_all) {
         cx.last_kernel = 4;
         cx.last_ksplit = 1;
         return launch_x3h(q, stream, x3h_tiles, cx.x3_spread);

@@ -278,6 +278,13 @@ class ScoreModel(nn.Module):
         # the checkpoint's data-module hparams pick the front / back end (_forward_transform(_stft(.)),
         # model.py:749, to_audio 612-613): fused exponent transform or raw, anything else raises
         mode = self.data_module.hip_mode()
+        if self.snr_conditioned == "fixed":
+            # model.py:792-793: the reference refuses inference for this training-only mode (it raises after
+            # the STFT, before any network call; here before any device work)
+            raise NotImplementedError("snr fixed is only for experiment purpose, not real inference.")
+        if self.snr_conditioned not in ("true", "false"):
+            # the reference falls through every branch and fails on the unbound `sample` (model.py:826)
+            raise NotImplementedError(f"snr_conditioned={self.snr_conditioned!r} has no enhance branch")
         dev = torch.device("cuda", torch.cuda.current_device())
         T_orig = y.size(1)
         yd = y.to(dev, torch.float32).reshape(1, -1).contiguous()

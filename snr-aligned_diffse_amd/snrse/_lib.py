@@ -71,7 +71,7 @@ SIGNATURES = {
     "snrse_ct_loss": [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp],
     "snrse_adam_ema": [_vp, _vp, _vp, _i, _f, _f, _f, _f, _f, _f, _f, _vp],
 }
-HOUSEKEEPING = {"snrse_abi_version": ([], _i), "snrse_error_string": ([_i], C.c_char_p),
+HOUSEKEEPING = {"snrse_abi_version": ([], _i), "snrse_build_id": ([], C.c_char_p), "snrse_error_string": ([_i], C.c_char_p),
                 "snrse_device_name": ([C.c_char_p, _i], _i), "snrse_snrnet_workspace": ([_i, _i], C.c_size_t),
                 "snrse_ctx_create": ([], _vp), "snrse_ctx_destroy": ([_vp], None)}
 

@@ -8,8 +8,10 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import subprocess
+import time
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(PKG, "csrc")
@@ -34,11 +36,31 @@ def _headers(csrc=CSRC):
     return glob.glob(os.path.join(csrc, "*.h"))
 
 
+def source_hash(csrc=CSRC) -> str:
+    """sha256 over the library's sources (csrc/*.hip, *.cpp, *.h) and this build script, by content:
+    compiled into the library as snrse_build_id() and written beside it as libsnrse_hip.so.id."""
+    h = hashlib.sha256()
+    for f in sorted(_sources(csrc) + _headers(csrc), key=os.path.basename) + [os.path.abspath(__file__)]:
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+# what the latest build_library() call did (printed by __graft_entry__.build())
+LAST_BUILD = {"compiled": False, "build_id": None, "seconds": 0.0, "lib": LIB}
+
+
 def needs_build() -> bool:
+    """The library is rebuilt unless it exists and its recorded source hash equals the tree's (content,
+    not mtimes: a checkout or a copy that touches no bytes does not rebuild, an edit always does)."""
     if not os.path.exists(LIB):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(f) > t for f in _sources() + _headers() + [os.path.abspath(__file__)])
+    try:
+        with open(LIB + ".id") as f:
+            return f.read().strip() != source_hash()
+    except OSError:
+        return True
 
 
 def _compile(src: str, obj: str, extra=()):
@@ -53,8 +75,11 @@ def build_library(force: bool = False, jobs: int = 8, extra_flags=(), lib: str =
     """Build `lib`.  `extra_flags` (e.g. -DSNRSE_STAMPS for the timing-diagnostic build) go to
     every compile; such builds use their own object directory next to `lib`.  `csrc` selects another
     source tree (A/B builds of an earlier revision, tools/build_variant.py)."""
+    bid = source_hash(csrc)
+    LAST_BUILD.update(compiled=False, build_id=bid, seconds=0.0, lib=lib)
     if lib == LIB and not force and not needs_build():
         return LIB
+    t0 = time.time()
     objdir = os.path.join(os.path.dirname(lib), "obj")
     os.makedirs(objdir, exist_ok=True)
     hdr_t = max([os.path.getmtime(h) for h in _headers(csrc) + [os.path.abspath(__file__)]] + [0.0])
@@ -62,10 +87,14 @@ def build_library(force: bool = False, jobs: int = 8, extra_flags=(), lib: str =
     for src in _sources(csrc):
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
         objs.append(obj)
-        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_t):
+        if (force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_t)
+                or os.path.basename(src) == "abi.cpp"):  # abi.cpp carries the build id: always recompiled
             todo.append((src, obj))
+    idflag = (f'-DSNRSE_BUILD_ID="{bid}"',)
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo) or 1))) as ex:
-        for f in [ex.submit(_compile, s, o, tuple(extra_flags)) for s, o in todo]:
+        futs = [ex.submit(_compile, s, o, tuple(extra_flags) + (idflag if os.path.basename(s) == "abi.cpp" else ()))
+                for s, o in todo]
+        for f in futs:
             f.result()
     tmp = lib + ".tmp"
     r = subprocess.run([HIPCC, "-shared", f"--offload-arch={ARCH}", *objs, "-o", tmp],
@@ -73,6 +102,9 @@ def build_library(force: bool = False, jobs: int = 8, extra_flags=(), lib: str =
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
     os.replace(tmp, lib)
+    with open(lib + ".id", "w") as f:
+        f.write(bid + "\n")
+    LAST_BUILD.update(compiled=True, seconds=round(time.time() - t0, 1))
     return lib
 
 

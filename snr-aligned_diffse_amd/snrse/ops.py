@@ -93,7 +93,8 @@ class LaunchContext:
         self.ws, mb = _ws_alloc(self.device)
         _lib.call("snrse_ctx_set_workspace", self.ptr, None if self.ws is None else self.ws.data_ptr(),
                   0 if self.ws is None else mb << 20)
-        self.zeroed = 0  # mirror of the context's "stats_zeroed" switch
+        # mirror of the context's "stats_zeroed" switch; snrse_ctx_create copies it from the process default
+        self.zeroed = int(bool(self.get_option("stats_zeroed")))
         self.seq = next(_CTX_SEQ)  # creation order (probe_read over several threads' contexts)
         _CONTEXTS.add(self)
 

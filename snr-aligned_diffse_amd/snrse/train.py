@@ -645,9 +645,15 @@ class FusedAdam(torch.optim.Optimizer):
                 by_step.setdefault(int(self.state[p]["step"]), []).append(p)
             keep = []
             for step, sub in by_step.items():
-                key = tuple(id(p) for p in sub)
-                if key not in self._chunk_cache:
+                # chunk tables depend only on the element counts, in order (a recycled id() cannot serve a
+                # table of other sizes); a few entries at most, oldest evicted (gradient presence can vary)
+                key = (str(sub[0].device),) + tuple(p.numel() for p in sub)
+                if key in self._chunk_cache:
+                    self._chunk_cache[key] = self._chunk_cache.pop(key)  # most recently used last
+                else:
                     self._chunk_cache[key] = self._chunks(sub)
+                    while len(self._chunk_cache) > 8:
+                        self._chunk_cache.pop(next(iter(self._chunk_cache)))
                 tix, starts = self._chunk_cache[key]
                 rec = np.zeros((len(sub), 6), dtype=np.int64)
                 for i, p in enumerate(sub):

@@ -151,6 +151,21 @@ def test_enhance_follows_data_module_transform():
         m.enhance(torch.zeros(1, 1000), torch.zeros(1, 1000))
 
 
+def test_enhance_fixed_snr_branch_raises_like_reference():
+    """snr_conditioned='fixed' is a training-only mode: the reference's enhance raises
+    NotImplementedError("snr fixed is only for experiment purpose, not real inference.")
+    (sgmse-bbed/sgmse/model.py:792-793); here it raises the same, before any device work, while the
+    model itself still constructs (the 'fixed' consistency-training branch needs it)."""
+    from sgmse.model import ScoreModel
+    m = ScoreModel(backbone="ncsnpp", sde="ouve", model_type="sebridge_v3", snr_conditioned="fixed",
+                   fixed_snr=0.17783, theta=1.5, sigma_min=0.05, sigma_max=0.5)
+    with pytest.raises(NotImplementedError, match="snr fixed is only for experiment purpose, not real inference."):
+        m.enhance(torch.zeros(1, 16000), torch.zeros(1, 16000))
+    m.snr_conditioned = "bogus"
+    with pytest.raises(NotImplementedError):
+        m.enhance(torch.zeros(1, 16000), torch.zeros(1, 16000))
+
+
 def test_upfirdn2d_dtype_table():
     """The reference binding dispatches float / double / half (upfirdn2d_kernel.cu:311)."""
     from snrse import _lib, ops
