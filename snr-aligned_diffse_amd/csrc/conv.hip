@@ -1782,6 +1782,18 @@ int dispatch_conv(const ConvParams& p, hipStream_t s, snrse_ctx& cx) {
         // halo path on the 4 x 64-tileable images (levels 0-3 of the C2 pyramid), with 8 x 32 tiles where
         // H % 8 == 0.  Not on W = 32 (level 4): 128 tiles for 512 workgroup slots ran 11-45 % slower there
         // than the split-K LDS-DMA GEMM + gn_act (profiles/r03v_level4_halo_vs_glds.jsonl)
+        if constexpr (sizeof(TO) == 2) {
+          // v10 (conv_h10.hip): forced by conv_variant 10, taken by variant 0 under option h10
+          if ((cx.conv_variant == 10 || (cx.conv_variant == 0 && cx.h10)) && h10_ok(p)) {
+            if (!cx.num_cu) {
+              int dev = 0;
+              SNRSE_RET(hipGetDevice(&dev));
+              SNRSE_RET(hipDeviceGetAttribute(&cx.num_cu, hipDeviceAttributeMultiprocessorCount, dev));
+            }
+            cx.last_kernel = 12;
+            return launch_h10(p, s, cx.num_cu, cx.h5_specialise != 0);
+          }
+        }
         if (cx.conv_variant != 2 && p.ksize == 3 && halo_tile64(p)) {
           cx.last_kernel = kHaloAuto;
           return launch_halo5<TO>(p, s, cx);
