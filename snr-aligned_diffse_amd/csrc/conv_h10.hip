@@ -16,8 +16,13 @@
 //     one tap ahead; halo fragments are read from LDS four 16-px blocks ahead, across tap boundaries;
 //   * one barrier per chunk (the halo buffers swap); the 512-px tile has 612 halo rows (1.20 x the tile, against
 //     1.33 x for v5's 256-px tiles), so there is 10 % less GroupNorm+SiLU work per output.
-// Shapes: H % 16 == 0, W % 32 == 0, Cout % 128 == 0, no fused 1x1 shortcut (those stay on v5).
+//   * a fused 1x1 shortcut (Conv_2 as extra K, layerspp.py:268-274) runs as one-tap chunks over an unpadded pixel
+//     tile (512 rows x 64 B) in two more LDS buffers: up to two such chunks right before each main chunk, their tiles
+//     loaded during the previous main chunk (so at most 2 shortcut chunks per main chunk: nsc <= 2 ncb).
+// Shapes: H % 16 == 0, W % 32 == 0, Cout % 128 == 0, shortcut channels <= 2 x main channels.
 #include "conv_common.h"
+
+#include <utility>
 
 using namespace snrse_conv;
 
@@ -27,8 +32,48 @@ constexpr int TH = 16, TW = 32, HC = TW + 2;
 constexpr int HROWS = (TH + 2) * HC;     // 612
 constexpr int HBYTES = HROWS * 64;       // 39168
 constexpr int VPT = (HROWS * 4 + 255) / 256;  // 10 halo vectors (16 B) per thread: vector tid + 256 k
-constexpr int LDS = 2 * HBYTES;
+constexpr int SCBYTES = TH * TW * 64;  // a shortcut chunk's pixel tile (no halo): 512 rows x 64 B
+constexpr int SCOFF = 2 * HBYTES;       // two halo buffers, then two shortcut tiles
+constexpr int SCV = TH * TW * 4 / 256;  // 8 shortcut vectors per thread per chunk
+constexpr int LDS = 2 * HBYTES + 2 * SCBYTES;  // 143,872 B
 constexpr int KT = 32;
+// the next chunk's halo, vector k (k = 0 .. VPT-1): loaded at 16-px step LOAD0 + STRIDE k (a step = 4 MFMAs),
+// transformed over NSLOT consecutive steps from XF0 + STRIDE k (one slice of VALU work beside each MFMA), stored at
+// the end of its last slot; 9 taps x 16 steps = 144 steps per chunk
+constexpr int STRIDE = 10, XF0 = 40, LOAD0 = XF0 - 32;
+static_assert(XF0 + STRIDE * (VPT - 1) + 9 <= 144, "transform schedule fits one chunk");
+// up to two shortcut chunks' tiles (2 x 8 vectors per thread) loaded every SCSTRIDE steps from SCL0, stored SCLAG later
+constexpr int SCSTRIDE = 6, SCL0 = 4, SCLAG = 30;
+static_assert(SCL0 + SCSTRIDE * 15 + SCLAG < 144, "shortcut schedule fits one chunk");
+
+// single VALU instructions as asm statements: with the MFMAs also in asm (program order of volatile asm is kept),
+// the interleave below is the issue order -- the compiler neither hoists the transform into a VALU-only block nor
+// moves it across the MFMAs (operands are registers only; no wait states needed between these and the MFMAs)
+SNRSE_DEV float a_lshl16(uint32_t s) { float d; asm volatile("v_lshlrev_b32 %0, 16, %1" : "=v"(d) : "v"(s)); return d; }
+SNRSE_DEV float a_andhi(uint32_t s) { float d; asm volatile("v_and_b32 %0, 0xffff0000, %1" : "=v"(d) : "v"(s)); return d; }
+SNRSE_DEV void a_fma(float& d, float b, float c) { asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(d) : "v"(b), "v"(c)); }
+SNRSE_DEV float a_exp(float s) { float d; asm volatile("v_exp_f32 %0, %1" : "=v"(d) : "v"(s)); return d; }
+// e * (-1/ln2) + (-1/ln2): 0xbfb8aa3b = -log2(e) = -1/ln(2) (kNegInvLn2), k holds the same value
+SNRSE_DEV void a_fmamk(float& d, float k) { asm volatile("v_fmamk_f32 %0, %0, 0xbfb8aa3b, %1" : "+v"(d) : "v"(k)); }
+SNRSE_DEV void a_rcp(float& d) { asm volatile("v_rcp_f32 %0, %0" : "+v"(d)); }
+SNRSE_DEV void a_mul(float& d, float s) { asm volatile("v_mul_f32 %0, %0, %1" : "+v"(d) : "v"(s)); }
+SNRSE_DEV uint32_t a_cvtpk(float a, float b) {
+  uint32_t d;
+  asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+SNRSE_DEV void a_and(uint32_t& d, uint32_t m) { asm volatile("v_and_b32 %0, %0, %1" : "+v"(d) : "v"(m)); }
+template <int N, typename F, int... S>
+SNRSE_DEV void static_for_impl(F&& f, std::integer_sequence<int, S...>) {
+  (f(std::integral_constant<int, S>{}), ...);
+}
+template <int N, typename F>
+SNRSE_DEV void static_for(F&& f) {
+  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
+}
+SNRSE_DEV void a_mfma(f32x4& acc, const u32x4& w, const u32x4& h) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(w), "v"(h));
+}
 }  // namespace h10
 
 template <int GNM, int EF>
@@ -50,14 +95,21 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
   const int H = p.H, W = p.W;
   const int ntw = W / TW, nth = H / TH;
   const int Cin = p.C0 + p.C1, ncb = Cin / KT, K1 = 9 * Cin;
+  // fused 1x1 shortcut (Conv_2 as extra K): nsc chunks of 32 channels, the ones of group m (sb(m) .. sb(m + 1) - 1,
+  // at most 2) run right before main chunk m, their pixel tiles prepared during main chunk m - 1
+  const int Csc_all = p.sc_src ? p.Csc + p.Csc1 : 0, nsc = Csc_all / KT;
+  auto sb = [&](int m) { return m * nsc / ncb; };
   const bool f_temb = EF < 0 ? p.temb != nullptr : (EF & EF_TEMB) != 0;
   const bool f_res = EF < 0 ? p.res != nullptr : (EF & EF_RES) != 0;
   const bool f_comb = EF < 0 ? p.comb_src != nullptr : (EF & EF_COMB) != 0;
   const bool f_stats = EF < 0 ? p.stats != nullptr : (EF & EF_STATS) != 0;
 
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.wgt, p.wbytes);
+  const __amdgpu_buffer_rsrc_t rws = make_rsrc(nsc ? p.sc_wgt : p.wgt, nsc ? p.sc_wbytes : p.wbytes);
   const __amdgpu_buffer_rsrc_t rs0 = make_rsrc(p.src0, p.bytes0);
   const __amdgpu_buffer_rsrc_t rs1 = make_rsrc(p.C1 ? p.src1 : p.src0, p.C1 ? p.bytes1 : p.bytes0);
+  const __amdgpu_buffer_rsrc_t rc0 = make_rsrc(nsc ? p.sc_src : p.src0, nsc ? p.sc_bytes0 : p.bytes0);
+  const __amdgpu_buffer_rsrc_t rc1 = make_rsrc(p.Csc1 && nsc ? p.sc_src1 : p.src0, p.Csc1 && nsc ? p.sc_bytes1 : p.bytes0);
 
   // ---- halo fragment addresses: row hr of a buffer at hr * 64 + ((lg ^ ((hr >> 1) & 3)) << 4).  Fragment i of tap
   // (dy, dx) reads row R0 + k with R0 = ph * 8 * HC + lrow and k = ((i >> 1) + dy + 1) * HC + (i & 1) * 16 + dx + 1;
@@ -69,6 +121,8 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
     const int r = ph * 8 * HC + lrow + m;
     hb[m] = r * 64 + ((lg ^ ((r >> 1) & 3)) << 4);
   }
+  // shortcut tile rows: pixel block i of the wave = rows ph * 256 + 16 i + lrow, swizzle (lrow >> 1) & 3
+  const int scb = SCOFF + (ph * 256 + lrow) * 64 + ((lg ^ ((lrow >> 1) & 3)) << 4);
 
   // ---- per-thread halo vectors of a tile: row (tid >> 2) + 64 k, 16-B chunk tid & 3 (8 channels)
   const int hcol = tid & 3;
@@ -82,6 +136,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
     hyx[k] = hr < HROWS ? hy * 64 + (hr - hy * HC) : 63 * 64;
   }
   int hpix[VPT];
+  int spix = 0;  // shortcut tile: pixel of this thread's vector r = 0 (vector r: + 2 r W)
   auto halo_geom = [&](int b, int h0, int w0) {
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
@@ -89,6 +144,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
       const bool ok = ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
       hpix[k] = ok ? (b * H + ih) * W + iw : -1;
     }
+    spix = (b * H + h0 + (tid >> 7)) * W + w0 + ((tid >> 2) & 31);
   };
   auto tile_coords = [&](int t, int& n0, int& b, int& h0, int& w0) {
     n0 = (t % p.ntn) * 128;
@@ -99,15 +155,19 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
     b = t / nth;
   };
 
-  // ---- state of the chunk being prepared (the "next" chunk)
+  // ---- state of the group being prepared: its shortcut chunks (first pu0, count pn) and its main chunk pc
   u32x4 hv[VPT];
+  u32x4 sv[2 * SCV];
   float gsc[8], gsh[8];
-  int pc_ch = 0;      // its first channel
+  int pc_ch = 0;       // first channel of the main chunk
   bool pc_src1 = false;
-  int pc_buf = 0;     // LDS buffer it goes to
-  auto prep_begin = [&](int c, int b) {  // chunk c of the tile whose geometry is in hpix / hok
+  int pc_buf = 0;      // halo buffer it goes to
+  int pu0 = 0, pn = 0;
+  auto prep_begin = [&](int c, int b) {  // main chunk c of the tile whose geometry is in hpix / spix
     pc_ch = c * KT;
     pc_src1 = pc_ch >= p.C0;
+    pu0 = sb(c);
+    pn = sb(c + 1) - pu0;
     if constexpr (GNM > 0) {
       const float* s = p.gn_scale + (size_t)b * Cin + pc_ch + hcol * 8;
       const float* t = p.gn_shift + (size_t)b * Cin + pc_ch + hcol * 8;
@@ -127,26 +187,78 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
     const int voff = hpix[k] >= 0 ? (hpix[k] * cs + cc) * 2 : (int)0x80000000;
     hv[k] = __builtin_amdgcn_raw_buffer_load_b128(pc_src1 ? rs1 : rs0, voff, 0, 0);
   };
-  auto prep_store = [&](int k) {
+  auto prep_store = [&](int k) {  // (prologue: the whole transform at once)
     const int hr = (tid >> 2) + 64 * k;
     if (k == VPT - 1 && hr >= HROWS) return;
     u32x4 v = hv[k];
     if constexpr (GNM > 0) v = gn_xform8<GNM>(v, gsc, gsh, hpix[k] >= 0);
     *(u32x4*)(smem + pc_buf * HBYTES + swz64(hr, hcol)) = v;
   };
+  // shortcut vector q of the group: chunk pu0 + q / SCV, tile row (tid >> 2) + 64 (q % SCV); no transform (raw x)
+  auto sc_load = [&](int q) {
+    // (always issued -- past the group's last shortcut chunk it re-reads its first one, a valid address -- so sv[q] is
+    // defined on every path and no shortcut vector stays live across the loops)
+    const int ch = (q / SCV < pn ? pu0 + q / SCV : pu0) * KT;
+    const bool one = ch >= p.Csc;
+    const int cs = one ? p.Csc1 : p.Csc;
+    const int pix = spix + 2 * (q % SCV) * W;
+    sv[q] = __builtin_amdgcn_raw_buffer_load_b128(one ? rc1 : rc0, (pix * cs + (one ? ch - p.Csc : ch) + hcol * 8) * 2, 0, 0);
+  };
+  auto sc_store = [&](int q) {
+    if (q / SCV >= pn) return;
+    *(u32x4*)(smem + SCOFF + (q / SCV) * SCBYTES + swz64((tid >> 2) + 64 * (q % SCV), hcol)) = sv[q];
+  };
+  // the transform in slots beside the MFMAs of one 16-px step each (xf_slice(step, mfma j) emits the VALU that
+  // follows MFMA j): GNM 2: unpack, affine, exp x2, fma, rcp x2, mul, pack + mask (9 slots); GNM 1: unpack, affine,
+  // pack + mask; GNM 0: the raw vector is stored (its padding is zero already: out-of-range buffer loads read 0)
+  constexpr int NSLOT = GNM == 2 ? 9 : GNM == 1 ? 3 : 1;
+  float xy[8], xe[8];
+  uint32_t xo[4];
+  const float knl2 = kNegInvLn2;
+  // slice (ST, J): the VALU issued after MFMA J of step ST (compile-time: every index is a constant)
+  auto xf_slice = [&](auto ST, auto J) {
+    constexpr int st = decltype(ST)::value, j = decltype(J)::value;
+    if constexpr (GNM > 0 && st >= XF0 && (st - XF0) % STRIDE < NSLOT && (st - XF0) / STRIDE < VPT) {
+      constexpr int k = (st - XF0) / STRIDE, sl = (st - XF0) % STRIDE;
+      constexpr int slot = GNM == 2 ? sl : (sl == 2 ? 8 : sl);  // GNM 1: unpack, affine, pack
+      constexpr int e0 = 2 * j, e1 = 2 * j + 1;
+      if constexpr (slot == 0) { xy[e0] = a_lshl16(hv[k][j]); xy[e1] = a_andhi(hv[k][j]); }
+      if constexpr (slot == 1) { a_fma(xy[e0], gsc[e0], gsh[e0]); a_fma(xy[e1], gsc[e1], gsh[e1]); }
+      if constexpr (slot == 2) xe[j] = a_exp(xy[j]);
+      if constexpr (slot == 3) xe[4 + j] = a_exp(xy[4 + j]);
+      if constexpr (slot == 4) { a_fmamk(xe[e0], knl2); a_fmamk(xe[e1], knl2); }
+      if constexpr (slot == 5) a_rcp(xe[j]);
+      if constexpr (slot == 6) a_rcp(xe[4 + j]);
+      if constexpr (slot == 7) { a_mul(xy[e0], xe[e0]); a_mul(xy[e1], xe[e1]); }
+      if constexpr (slot == 8) {
+        xo[j] = a_cvtpk(xy[e0], xy[e1]);
+        a_and(xo[j], hpix[k] >= 0 ? 0xffffffffu : 0u);  // the conv's zero padding
+      }
+    }
+  };
+  auto xf_store = [&](int k) {
+    const int hr = (tid >> 2) + 64 * k;
+    u32x4 v;
+    if constexpr (GNM > 0) v = u32x4{xo[0], xo[1], xo[2], xo[3]};
+    else v = hv[k];
+    if (k < VPT - 1 || hr < HROWS) *(u32x4*)(smem + pc_buf * HBYTES + swz64(hr, hcol)) = v;
+  };
 
-  // ---- weight fragments (A operand): cout row n0 + chh * 64 + 16 j + lrow, 8 channels at lg * 8 of K offset koff
-  auto wload = [&](u32x4 (&wf)[4], int n0, int tap, int c) {
-    const int vb = ((n0 + chh * 64 + lrow) * K1 + lg * 8) * 2;
-    const int koff = (tap * Cin + c * KT) * 2;
+  // ---- weight fragments (A operand): cout row n0 + chh * 64 + 16 j + lrow, 8 channels at lg * 8 of K offset koff;
+  // main chunk c, tap t: [Cout][9 Cin] at t Cin + 32 c; shortcut chunk u: [Cout][Csc_all] at 32 u
+  auto wload = [&](u32x4 (&wf)[4], int n0, bool sc, int tap, int c) {
+    const int ld = sc ? Csc_all : K1;
+    const int vb = ((n0 + chh * 64 + lrow) * ld + lg * 8) * 2;
+    const int koff = ((sc ? 0 : tap * Cin) + c * KT) * 2;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) wf[j] = __builtin_amdgcn_raw_buffer_load_b128(rw, vb, j * 16 * K1 * 2 + koff, 0);
+    for (int j = 0; j < 4; ++j)
+      wf[j] = __builtin_amdgcn_raw_buffer_load_b128(sc ? rws : rw, vb, j * 16 * ld * 2 + koff, 0);
   };
 
   f32x4 acc[16][4];
   u32x4 wcur[4], wnext[4];
 
-  // ---- prologue: the first tile's chunk 0 halo, synchronously
+  // ---- prologue: the first tile's group 0 (shortcut chunks + main chunk 0), synchronously
   int n0, bb, h0, w0;
   tile_coords(t_begin, n0, bb, h0, w0);
   halo_geom(bb, h0, w0);
@@ -155,9 +267,13 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
 #pragma unroll
   for (int k = 0; k < VPT; ++k) prep_load(k);
 #pragma unroll
+  for (int q = 0; q < 2 * SCV; ++q) sc_load(q);
+#pragma unroll
   for (int k = 0; k < VPT; ++k) prep_store(k);
-  wload(wnext, n0, 0, 0);
-  int gc = 0;  // chunks done by this workgroup (buffer parity)
+#pragma unroll
+  for (int q = 0; q < 2 * SCV; ++q) sc_store(q);
+  wload(wnext, n0, pn > 0, 0, pn > 0 ? pu0 : 0);
+  int gc = 0;  // main chunks done by this workgroup (halo buffer parity)
 
   for (int t = t_begin; t < t_end; ++t) {
     tile_coords(t, n0, bb, h0, w0);
@@ -167,22 +283,52 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     int nn0 = n0;  // cout tile of the weights loaded for the next tap
     for (int c = 0; c < ncb; ++c) {
-      // the chunk prepared during this one: c + 1 of this tile, or chunk 0 of the next tile
+      // ---- the shortcut chunks of group c (their tiles in the two shortcut buffers), one tap each
+      const int u_end = sb(c + 1);
+      for (int u = sb(c); u < u_end; ++u) {
+        const int sbuf = u - sb(c);
+        const bool nxt_sc = u + 1 < u_end;  // the next chunk: shortcut u + 1, else main chunk c (tap 0)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        u32x4 sf[16];
+        auto sread = [&](int i) { sf[i] = *(const u32x4*)(smem + scb + sbuf * SCBYTES + i * 1024); };
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sread(i);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wcur[j] = wnext[j];
+        wload(wnext, n0, nxt_sc, 0, nxt_sc ? u + 1 : c);
+        static_for<16>([&](auto I) {
+          constexpr int i = decltype(I)::value;
+          if constexpr (i + 4 < 16) sread(i + 4);
+          static_for<4>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            if constexpr (i == 0 && j == 0) asm volatile("s_nop 1" ::: "memory");
+            a_mfma(acc[i][j], wcur[j], sf[i]);
+          });
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      }
+      // ---- main chunk c; prepared meanwhile: group c + 1 of this tile, or group 0 of the next tile; after the
+      // workgroup's last chunk, a dummy one (every vector out of range: zeros into free buffers, read by nobody), so
+      // the step sequence below has no branches
       const bool last_c = c + 1 == ncb;
-      const bool has_next = !last_c || t + 1 < t_end;
       int pb = bb;
-      if (last_c && has_next) {
-        int h0n, w0n;
-        tile_coords(t + 1, nn0, pb, h0n, w0n);
-        halo_geom(pb, h0n, w0n);  // (this chunk's halo is already in LDS)
+      if (last_c) {
+        if (t + 1 < t_end) {
+          int h0n, w0n;
+          tile_coords(t + 1, nn0, pb, h0n, w0n);
+          halo_geom(pb, h0n, w0n);  // (this chunk's halo is already in LDS)
+        } else {
+#pragma unroll
+          for (int k = 0; k < VPT; ++k) hpix[k] = -1;
+        }
       }
-      if (has_next) {
-        prep_begin(last_c ? 0 : c + 1, pb);
-        pc_buf = (gc + 1) & 1;
-      }
-      const int nc = last_c ? 0 : c + 1;  // chunk of the weights prefetched at tap 8
+      prep_begin(last_c ? 0 : c + 1, pb);
+      pc_buf = (gc + 1) & 1;
+      const bool nsc_next = pn > 0;  // the chunk after this one: the next group's first shortcut chunk, or its main chunk
+      const int nc = nsc_next ? pu0 : (last_c ? 0 : c + 1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // halo(c) complete in buffer gc & 1; the other buffer is free
+      __builtin_amdgcn_s_barrier();  // halo(c) complete in buffer gc & 1; the other buffer and the shortcut tiles free
       const int boff = (gc & 1) * HBYTES;
       int hbc[8];
 #pragma unroll
@@ -195,36 +341,43 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
       };
 #pragma unroll
       for (int i = 0; i < 4; ++i) hread(0, i);
+      // 9 taps x 16 steps; step (tap, i): the halo fragment 4 steps ahead, then 4 MFMAs (pixel block i x the 4
+      // cout blocks), each followed by its slice of the next chunk's halo work
+      static_for<144>([&](auto ST) {
+        constexpr int st = decltype(ST)::value, tap = st / 16, i = st % 16;
+        if constexpr (i == 0) {
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) wcur[j] = wnext[j];
-        if (tap < 8) wload(wnext, n0, tap + 1, c);
-        else if (has_next) wload(wnext, nn0, 0, nc);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          if (i + 4 < 16) hread(tap, i + 4);
-          else if (tap < 8) hread(tap + 1, i - 12);
-          // the next chunk's halo: vector k loaded at tap k / 2, transformed + stored two taps later
-          if (has_next) {
-            if (i == 0 && tap < 5) prep_load(2 * tap);
-            if (i == 8 && tap < 5) prep_load(2 * tap + 1);
-            if (i == 4 && tap >= 2 && tap < 7) prep_store(2 * (tap - 2));
-            if (i == 12 && tap >= 2 && tap < 7) prep_store(2 * (tap - 2) + 1);
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            // inline asm with the accumulator tied in AGPRs: the builtin's register allocation rotates a third of
-            // the 256 accumulators through copies and spills (no spare AGPR quad); operands come from loads only
-            if (i == 0 && j == 0)  // (2 wait states after any compiler VALU write of an operand, e.g. a copy)
-              asm volatile("s_nop 1\n\tv_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(wcur[j]), "v"(hf[tap][i]));
-            else
-              asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(wcur[j]), "v"(hf[tap][i]));
-          // program order at 16-px-block granularity: the prefetch distances above are the schedule (the
-          // scheduler would otherwise hoist the fragment reads of the whole chunk and spill)
-          __builtin_amdgcn_sched_barrier(0);
+          for (int j = 0; j < 4; ++j) wcur[j] = wnext[j];
+          if constexpr (tap < 8) wload(wnext, n0, false, tap + 1, c);
+          else wload(wnext, nn0, nsc_next, 0, nc);
         }
-      }
+        if constexpr (i + 4 < 16) hread(tap, i + 4);
+        else if constexpr (tap < 8) hread(tap + 1, i - 12);
+        if constexpr (st >= LOAD0 && (st - LOAD0) % STRIDE == 0 && (st - LOAD0) / STRIDE < VPT) {
+          prep_load((st - LOAD0) / STRIDE);
+        }
+        if constexpr (st >= SCL0 && (st - SCL0) % SCSTRIDE == 0 && (st - SCL0) / SCSTRIDE < 2 * SCV) {
+          sc_load((st - SCL0) / SCSTRIDE);
+        }
+        static_for<4>([&](auto J) {
+          constexpr int j = decltype(J)::value;
+          if constexpr (i == 0 && j == 0)  // 2 wait states after any compiler VALU write of an operand (a copy)
+            asm volatile("s_nop 1" ::: "memory");
+          a_mfma(acc[i][j], wcur[j], hf[tap][i]);
+          xf_slice(ST, J);
+        });
+        if constexpr (st >= XF0 + NSLOT - 1 && (st - XF0 - NSLOT + 1) % STRIDE == 0 &&
+                      (st - XF0 - NSLOT + 1) / STRIDE < VPT) {
+          xf_store((st - XF0 - NSLOT + 1) / STRIDE);
+        }
+        if constexpr (st >= SCL0 + SCLAG && (st - SCL0 - SCLAG) % SCSTRIDE == 0 &&
+                      (st - SCL0 - SCLAG) / SCSTRIDE < 2 * SCV) {
+          sc_store((st - SCL0 - SCLAG) / SCSTRIDE);
+        }
+        // program order at step granularity: the prefetch distances above are the schedule (the scheduler would
+        // otherwise hoist the fragment reads of the whole chunk and spill)
+        __builtin_amdgcn_sched_barrier(0);
+      });
       ++gc;
     }
     // the asm MFMAs' results are read by the epilogue's v_accvgpr_read: wait states hipcc does not insert
@@ -249,60 +402,71 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
 #pragma unroll
       for (int e = 0; e < 4; ++e) add[j][e] = bv[e] + tv[e];
     }
-    float s1[4][4], s2[4][4];
+    // element pairs (e, e + 1) as float2: v_pk_add / v_pk_mul / v_pk_fma_f32 (two elements per VALU instruction; no
+    // MFMA runs beside the epilogue, where packed f32 would cost issue slots)
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    f32x2 s1[4][2], s2[4][2];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { s1[j][e] = 0.f; s2[j][e] = 0.f; }
+      for (int e = 0; e < 2; ++e) { s1[j][e] = f32x2{0.f, 0.f}; s2[j][e] = f32x2{0.f, 0.f}; }
     const int pix0 = (bb * H + h0 + ph * 8) * W + w0 + lrow;
     const float osc = p.out_scale;
+    auto epi = [&](auto SC) {  // SC: multiply by out_scale (a uniform branch outside the element loop)
+      constexpr bool scale = decltype(SC)::value;
+      const f32x2 osc2 = f32x2{osc, osc};
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int pix = pix0 + (i >> 1) * W + (i & 1) * 16;
-      f32x4 q = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (f_comb) q = *(const f32x4*)(p.comb_src + (size_t)pix * 4);
+      for (int i = 0; i < 16; ++i) {
+        const int pix = pix0 + (i >> 1) * W + (i & 1) * 16;
+        f32x4 q = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (f_comb) q = *(const f32x4*)(p.comb_src + (size_t)pix * 4);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int co = co0 + 16 * j;
-        float v[4];
+        for (int j = 0; j < 4; ++j) {
+          const int co = co0 + 16 * j;
+          f32x2 v[2];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] + add[j][e];
-        if (f_res) {
-          const uint2 rv = *(const uint2*)((const bf16_t*)p.res + (size_t)pix * p.res_ld + co);
-          v[0] += __uint_as_float(rv.x << 16);
-          v[1] += __uint_as_float(rv.x & 0xffff0000u);
-          v[2] += __uint_as_float(rv.y << 16);
-          v[3] += __uint_as_float(rv.y & 0xffff0000u);
-        }
-        if (osc != 1.f) {
+          for (int e = 0; e < 2; ++e)
+            v[e] = f32x2{acc[i][j][2 * e], acc[i][j][2 * e + 1]} + f32x2{add[j][2 * e], add[j][2 * e + 1]};
+          if (f_res) {
+            const uint2 rv = *(const uint2*)((const bf16_t*)p.res + (size_t)pix * p.res_ld + co);
+            v[0] += f32x2{__uint_as_float(rv.x << 16), __uint_as_float(rv.x & 0xffff0000u)};
+            v[1] += f32x2{__uint_as_float(rv.y << 16), __uint_as_float(rv.y & 0xffff0000u)};
+          }
+          if constexpr (scale) {
+            v[0] *= osc2;
+            v[1] *= osc2;
+          }
+          if (f_comb) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] *= osc;
-        }
-        if (f_comb) {
+            for (int e = 0; e < 4; ++e) {
+              const f32x4 cw = *(const f32x4*)(p.comb_w + (size_t)(co + e) * 4);
+              v[e >> 1][e & 1] += q[0] * cw[0] + q[1] * cw[1] + q[2] * cw[2] + q[3] * cw[3] + p.comb_b[co + e];
+            }
+          }
+          uint2 o;
+          o.x = pack_bf16x2(v[0][0], v[0][1]);
+          o.y = pack_bf16x2(v[1][0], v[1][1]);
+          *(uint2*)((bf16_t*)p.out + (size_t)pix * p.out_ld + co) = o;
+          if (f_stats) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const f32x4 cw = *(const f32x4*)(p.comb_w + (size_t)(co + e) * 4);
-            v[e] += q[0] * cw[0] + q[1] * cw[1] + q[2] * cw[2] + q[3] * cw[3] + p.comb_b[co + e];
+            for (int e = 0; e < 2; ++e) {
+              s1[j][e] += v[e];
+              s2[j][e] = v[e] * v[e] + s2[j][e];
+            }
           }
         }
-        uint2 o;
-        o.x = pack_bf16x2(v[0], v[1]);
-        o.y = pack_bf16x2(v[2], v[3]);
-        *(uint2*)((bf16_t*)p.out + (size_t)pix * p.out_ld + co) = o;
-        if (f_stats) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { s1[j][e] += v[e]; s2[j][e] = fmaf(v[e], v[e], s2[j][e]); }
-        }
+        __builtin_amdgcn_sched_barrier(0);  // one 16-px block at a time (the 256 accumulator reads are not hoisted)
       }
-      __builtin_amdgcn_sched_barrier(0);  // one 16-px block at a time (the 256 accumulator reads are not hoisted)
-    }
+    };
+    if (osc != 1.f) epi(std::integral_constant<bool, true>{});
+    else epi(std::integral_constant<bool, false>{});
     if (f_stats) {
       // sum over the 16 pixels of a lane row (lanes with equal lg): DPP row rotations
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float a = s1[j][e], q2 = s2[j][e];
+          float a = s1[j][e >> 1][e & 1], q2 = s2[j][e >> 1][e & 1];
           a += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x128, 0xf, 0xf, false));
           q2 += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(q2), 0x128, 0xf, 0xf, false));
           a += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x124, 0xf, 0xf, false));
@@ -311,8 +475,8 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
           q2 += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(q2), 0x122, 0xf, 0xf, false));
           a += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(a), 0x121, 0xf, 0xf, false));
           q2 += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(q2), 0x121, 0xf, 0xf, false));
-          s1[j][e] = a;
-          s2[j][e] = q2;
+          s1[j][e >> 1][e & 1] = a;
+          s2[j][e >> 1][e & 1] = q2;
         }
       if (lrow == 0) {
         const int slot = blockIdx.x & (SNRSE_STAT_SLOTS - 1);
@@ -321,8 +485,8 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const size_t o = stat_idx(bb, slot, co0 + 16 * j + e, p.Cout);
-            unsafeAtomicAdd(&p.stats[o], (double)s1[j][e]);
-            unsafeAtomicAdd(&p.stats[o + 1], (double)s2[j][e]);
+            unsafeAtomicAdd(&p.stats[o], (double)s1[j][e >> 1][e & 1]);
+            unsafeAtomicAdd(&p.stats[o + 1], (double)s2[j][e >> 1][e & 1]);
           }
       }
     }
@@ -356,7 +520,8 @@ int launch_h10_gn(const ConvParams& p, int ntiles, int grid, hipStream_t s, bool
 namespace snrse_conv {
 
 bool h10_ok(const ConvParams& p) {
-  return p.ksize == 3 && p.H % h10::TH == 0 && p.W % h10::TW == 0 && p.Cout % 128 == 0 && !p.sc_src && p.bias &&
+  const int ncb = (p.C0 + p.C1) / h10::KT, nsc = p.sc_src ? (p.Csc + p.Csc1) / h10::KT : 0;
+  return p.ksize == 3 && p.H % h10::TH == 0 && p.W % h10::TW == 0 && p.Cout % 128 == 0 && nsc <= 2 * ncb && p.bias &&
          (p.C0 + p.C1) % h10::KT == 0 && p.C0 % h10::KT == 0;
 }
 

@@ -19,7 +19,7 @@ def rel(a, b):
 
 
 CASES = [
-    # B, C0, C1, Cout, H, W, gn (0 none, 1 affine, 2 affine+SiLU), temb, res, comb, stats
+    # B, C0, C1, Cout, H, W, gn (0 none, 1 affine, 2 affine+SiLU), temb, res, comb, stats[, Csc, Csc1]
     (4, 128, 0, 128, 256, 512, 2, True, False, False, True),    # level-0 Conv_0 (1024 tiles)
     (4, 128, 0, 128, 256, 512, 2, False, True, False, True),    # level-0 Conv_1 + residual
     (8, 128, 128, 128, 128, 256, 2, True, False, False, True),  # up-path Conv_0 on cat(h, skip)
@@ -28,12 +28,18 @@ CASES = [
     (3, 128, 0, 128, 48, 96, 1, False, False, False, True),     # GroupNorm affine only; 27 tiles < CUs
     (7, 128, 0, 128, 128, 256, 2, False, True, True, True),     # Combine (run-time epilogue); 448 tiles
     (2, 128, 0, 128, 80, 96, 2, True, False, False, True),      # 30 tiles, H = 80
+    # fused 1x1 shortcut (Conv_2 as extra K, layerspp.py:268-274): shortcut chunks before every main chunk
+    (4, 128, 0, 128, 256, 512, 2, False, False, False, True, 128, 128),  # up-path Conv_1, level 0: 2 per main chunk
+    (4, 256, 0, 256, 64, 128, 2, False, False, False, True, 256, 128),   # 1.5 per main chunk, two cout tiles
+    (2, 256, 0, 256, 32, 64, 2, False, False, True, True, 128, 0),       # 0.5 per main chunk, Combine
+    (3, 128, 0, 128, 48, 96, 2, False, False, False, True, 128, 128),    # 27 tiles
 ]
 
 
 def _case(gpu, case):
     from snrse import ops
-    B, C0, C1, Co, H, W, gnm, use_temb, use_res, use_comb, use_st = case
+    B, C0, C1, Co, H, W, gnm, use_temb, use_res, use_comb, use_st = case[:11]
+    Csc, Csc1 = case[11:] if len(case) > 11 else (0, 0)
     g = torch.Generator(device=gpu).manual_seed(sum(case[:6]) + 7)
     Cin = C0 + C1
     x0 = (torch.randn(B, H, W, C0, device=gpu, generator=g) * 1.3 + 0.1).bfloat16()
@@ -45,6 +51,11 @@ def _case(gpu, case):
         kw.update(temb=torch.randn(B, Co + 40, device=gpu, generator=g), temb_off=40)
     if use_res:
         kw.update(res=torch.randn(B, H, W, Co, device=gpu, generator=g).bfloat16(), out_scale=1 / math.sqrt(2))
+    if Csc:
+        kw.update(sc=torch.randn(B, H, W, Csc, device=gpu, generator=g).bfloat16(),
+                  sc1=torch.randn(B, H, W, Csc1, device=gpu, generator=g).bfloat16() if Csc1 else None,
+                  sc_wgt=(torch.randn(Co, Csc + Csc1, device=gpu, generator=g) / math.sqrt(Csc + Csc1)).bfloat16(),
+                  out_scale=1 / math.sqrt(2))
     if use_comb:
         kw.update(comb=torch.randn(B, H, W, 4, device=gpu, generator=g), comb_w=torch.randn(Co, 4, device=gpu, generator=g),
                   comb_b=torch.randn(Co, device=gpu, generator=g))
@@ -61,6 +72,9 @@ def _case(gpu, case):
     ref = F.conv2d(a, w.float().permute(0, 3, 1, 2), bias, padding=1)
     if use_temb:
         ref = ref + kw["temb"][:, 40:40 + Co, None, None]
+    if Csc:
+        xs = kw["sc"] if not Csc1 else torch.cat([kw["sc"], kw["sc1"]], -1)
+        ref = (ref + torch.einsum("bhwc,oc->bohw", xs.float(), kw["sc_wgt"].float())) * kw["out_scale"]
     if use_res:
         ref = (ref + kw["res"].float().permute(0, 3, 1, 2)) * kw["out_scale"]
     if use_comb:
