@@ -1884,6 +1884,17 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
   auto run = [&](const ConvParams& q) {
     if (x3) {
       const int x3h_tiles = q.B * (q.H / x3h::TH) * ((q.W + x3h::TW - 1) / x3h::TW) * (q.Cout / 128);
+      // the v10 structure's split-bf16 form (option h10) where its 8 x 32 tiles fit; GroupNorm prologue or not
+      if (cx.h10 && h10x3_ok(q) && (x3h_all || !q.gn_scale)) {
+        if (!cx.num_cu) {
+          int dev = 0;
+          SNRSE_RET(hipGetDevice(&dev));
+          SNRSE_RET(hipDeviceGetAttribute(&cx.num_cu, hipDeviceAttributeMultiprocessorCount, dev));
+        }
+        cx.last_kernel = 13;
+        cx.last_ksplit = 1;
+        return launch_h10x3(q, stream, cx.num_cu);
+      }
       if (x3h_all) {
         cx.last_kernel = 4;
         cx.last_ksplit = 1;

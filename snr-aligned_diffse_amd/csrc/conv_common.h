@@ -95,6 +95,9 @@ int launch_head(const ConvParams& p, hipStream_t s);
 // v10 halo GEMM (conv_h10.hip): persistent, one wave per SIMD, 16 x 32 px x 128 cout tiles, no fused shortcut
 bool h10_ok(const ConvParams& p);
 int launch_h10(ConvParams p, hipStream_t s, int num_cu, bool specialise);
+// its split-bf16 form for the fp32x3 parity mode (conv_h10x3.hip): 8 x 32 px x 128 cout tiles
+bool h10x3_ok(const ConvParams& p);
+int launch_h10x3(ConvParams p, hipStream_t s, int num_cu);
 int launch_head_x3(const ConvParams& p, hipStream_t s);
 bool head_ok(const ConvParams& p);
 

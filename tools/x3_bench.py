@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--exact", type=int, default=1)
     ap.add_argument("--gn", type=int, default=0, help="1: fused GroupNorm+SiLU on the x3h variants (x3_tile 0)")
     ap.add_argument("--spread", default="1", help="x3_spread settings to run each split variant with")
+    ap.add_argument("--h10", type=int, default=0, help="1: also the v10 split kernel (option h10), with --gn fused")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
@@ -59,12 +60,15 @@ def main():
             sc = torch.rand(B, C0 + C1, device=dev, generator=g) + 0.5
             gn = (sc, torch.randn(B, C0 + C1, device=dev, generator=g) * 0.1)
             variants = [("x3gn", 0, sp) for sp in spreads] + variants
+        if args.h10:
+            variants = [("x3gn10" if args.gn else "x310", 0, 1)] + variants
         ref = None
         for kind, t, sp in variants:
             ops.set_option("x3_tile", t)
             ops.set_option("x3_spread", sp)
+            ops.set_option("h10", 1 if kind.endswith("10") else 0)
             wt = w if kind == "exact" else ws
-            kw = {"gn": gn} if kind == "x3gn" else {}
+            kw = {"gn": gn} if kind.startswith("x3gn") else {}
             fn = lambda: ops.conv2d(x0, wt, 3, Co, bias=b, src1=x1, out=out, stats=st, **kw)  # noqa: E731
             ms = time_call(fn, args.reps)
             fn()
@@ -78,6 +82,7 @@ def main():
                               "ksplit": ops.get_option("last_ksplit"), "rel_vs_first": err}), flush=True)
         ops.set_option("x3_tile", 0)
         ops.set_option("x3_spread", 1)
+        ops.set_option("h10", 0)
         del x0, x1, out, ref
 
 
