@@ -156,7 +156,7 @@ def pc_vs_golden(dev, net=None, dtype=torch.bfloat16):
 C2_AGREE = {"si_sdr_min_db": 25.0, "rel_rms_max": 5e-2}
 
 
-def waveform_agreement(est, ref):
+def waveform_agreement(est, ref, per_clip=False):
     """Per-utterance agreement of waveforms est [B, L] with ref [B, L] (float64): SI-SDR of est against ref as
     the reference computes it (sgmse/util/other.py:71-75: alpha = <est, ref> / |ref|^2, 10 log10 |alpha ref|^2 /
     |alpha ref - est|^2) and the relative RMS |est - ref| / |ref|; minimum / maximum over the batch."""
@@ -171,6 +171,10 @@ def waveform_agreement(est, ref):
     out["ok"] = bool(np.isfinite(out["si_sdr_bf16_vs_x3_db_min"]) and out["si_sdr_bf16_vs_x3_db_min"] >= C2_AGREE["si_sdr_min_db"]
                      and out["rel_rms_max"] <= C2_AGREE["rel_rms_max"])
     out["bounds"] = dict(C2_AGREE)
+    if per_clip:
+        out["per_clip"] = {"si_sdr_db": [round(float(v), 2) for v in sisdr],
+                           "rel_rms": [round(float(v), 4) for v in relr],
+                           "ref_rms": [float(v) for v in r.pow(2).mean(1).sqrt()]}
     return out
 
 

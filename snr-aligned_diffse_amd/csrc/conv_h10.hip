@@ -155,6 +155,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
     b = t / nth;
   };
 
+  int gc = -1;  // main chunks done by this workgroup (halo buffer parity); -1 in the prologue
   // ---- state of the group being prepared: its shortcut chunks (first pu0, count pn) and its main chunk pc
   u32x4 hv[VPT];
   u32x4 sv[2 * SCV];
@@ -185,6 +186,9 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
     const int cs = pc_src1 ? p.C1 : p.C0;
     const int cc = (pc_src1 ? pc_ch - p.C0 : pc_ch) + hcol * 8;
     const int voff = hpix[k] >= 0 ? (hpix[k] * cs + cc) * 2 : (int)0x80000000;
+#ifdef H10_EXP_NOHALOLOAD  // timing diagnostics only (results wrong): no halo loads after the prologue
+    if (gc >= 0) { hv[k] = u32x4{(uint32_t)voff, 0u, 0u, 0u}; return; }
+#endif
     hv[k] = __builtin_amdgcn_raw_buffer_load_b128(pc_src1 ? rs1 : rs0, voff, 0, 0);
   };
   auto prep_store = [&](int k) {  // (prologue: the whole transform at once)
@@ -202,6 +206,9 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
     const bool one = ch >= p.Csc;
     const int cs = one ? p.Csc1 : p.Csc;
     const int pix = spix + 2 * (q % SCV) * W;
+#ifdef H10_EXP_NOSCLOAD
+    if (gc >= 0) { sv[q] = u32x4{(uint32_t)pix, (uint32_t)ch, 0u, 0u}; return; }
+#endif
     sv[q] = __builtin_amdgcn_raw_buffer_load_b128(one ? rc1 : rc0, (pix * cs + (one ? ch - p.Csc : ch) + hcol * 8) * 2, 0, 0);
   };
   auto sc_store = [&](int q) {
@@ -218,7 +225,12 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
   // slice (ST, J): the VALU issued after MFMA J of step ST (compile-time: every index is a constant)
   auto xf_slice = [&](auto ST, auto J) {
     constexpr int st = decltype(ST)::value, j = decltype(J)::value;
-    if constexpr (GNM > 0 && st >= XF0 && (st - XF0) % STRIDE < NSLOT && (st - XF0) / STRIDE < VPT) {
+#ifdef H10_EXP_NOXF
+    if constexpr (false)
+#else
+    if constexpr (GNM > 0 && st >= XF0 && (st - XF0) % STRIDE < NSLOT && (st - XF0) / STRIDE < VPT)
+#endif
+    {
       constexpr int k = (st - XF0) / STRIDE, sl = (st - XF0) % STRIDE;
       constexpr int slot = GNM == 2 ? sl : (sl == 2 ? 8 : sl);  // GNM 1: unpack, affine, pack
       constexpr int e0 = 2 * j, e1 = 2 * j + 1;
@@ -250,6 +262,9 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
     const int ld = sc ? Csc_all : K1;
     const int vb = ((n0 + chh * 64 + lrow) * ld + lg * 8) * 2;
     const int koff = ((sc ? 0 : tap * Cin) + c * KT) * 2;
+#ifdef H10_EXP_NOWLOAD
+    if (gc >= 0) return;
+#endif
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       wf[j] = __builtin_amdgcn_raw_buffer_load_b128(sc ? rws : rw, vb, j * 16 * ld * 2 + koff, 0);
@@ -273,7 +288,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
 #pragma unroll
   for (int q = 0; q < 2 * SCV; ++q) sc_store(q);
   wload(wnext, n0, pn > 0, 0, pn > 0 ? pu0 : 0);
-  int gc = 0;  // main chunks done by this workgroup (halo buffer parity)
+  gc = 0;
 
   for (int t = t_begin; t < t_end; ++t) {
     tile_coords(t, n0, bb, h0, w0);

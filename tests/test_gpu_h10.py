@@ -99,12 +99,14 @@ def test_h10_vs_fp32_and_v5(gpu, case):
     from snrse import ops
     ref, run = _case(gpu, case)
     out10, st10, ran10 = run(10)
-    out5, st5, ran5 = run(5)
-    assert ran10 == "conv_halo10_kernel" and ran5 == "conv_halo5_kernel"
+    assert ran10 == "conv_halo10_kernel"
     got = out10.float().permute(0, 3, 1, 2)
     assert rel(got, ref) < 1e-2, rel(got, ref)
-    # v10 and v5 differ only in the fp32 accumulation order before the bf16 rounding
-    assert rel(out10.float(), out5.float()) < 4e-3
+    if case[5] % 64 == 0:  # (v5 tiles 64-px rows: no v5 leg at W = 96)
+        out5, st5, ran5 = run(5)
+        assert ran5 == "conv_halo5_kernel"
+        # v10 and v5 differ only in the fp32 accumulation order before the bf16 rounding
+        assert rel(out10.float(), out5.float()) < 4e-3
     if st10 is not None:
         o = out10.double()
         st_ref = torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)

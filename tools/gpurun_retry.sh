@@ -2,7 +2,7 @@
 # Re-submit a gpurun call only when the box could not be prepared (status "transient": nothing
 # ran, nothing charged).  Usage: tools/gpurun_retry.sh TIMEOUT 'command'
 T=$1; shift
-for i in 1 2 3 4 5 6 7 8; do
+for i in $(seq 1 ${RETRY_N:-8}); do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$@" > /tmp/gpurun_retry.out 2>&1
   rc=$?
   st=$(python3 -c "import json;print(json.load(open('/root/repo/gpurun_out/.last_call.json')).get('status'))" 2>/dev/null)
