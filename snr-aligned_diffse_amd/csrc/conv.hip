@@ -1791,7 +1791,10 @@ int dispatch_conv(const ConvParams& p, hipStream_t s, snrse_ctx& cx) {
               SNRSE_RET(hipDeviceGetAttribute(&cx.num_cu, hipDeviceAttributeMultiprocessorCount, dev));
             }
             cx.last_kernel = 12;
-            return launch_h10(p, s, cx.num_cu, cx.h5_specialise != 0);
+            ConvParams q = p;  // (non-temporal output stores as the v5 launch decides them)
+            q.epi_nt = cx.epi_nt == 2 ? ((long long)p.M * p.out_ld * 2ll > ((long long)cx.epi_nt_mb << 20)) : cx.epi_nt;
+            cx.last_epi_nt = q.epi_nt;
+            return launch_h10(q, s, cx.num_cu, cx.h5_specialise != 0);
           }
         }
         if (cx.conv_variant != 2 && p.ksize == 3 && halo_tile64(p)) {

@@ -76,7 +76,8 @@ SNRSE_DEV void a_mfma(f32x4& acc, const u32x4& w, const u32x4& h) {
 }
 }  // namespace h10
 
-template <int GNM, int EF>
+// SC: the launch has shortcut chunks (without: no shortcut registers or loads at all)
+template <int GNM, int EF, bool SC>
 __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int ntiles) {
   using namespace h10;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -97,12 +98,13 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
   const int Cin = p.C0 + p.C1, ncb = Cin / KT, K1 = 9 * Cin;
   // fused 1x1 shortcut (Conv_2 as extra K): nsc chunks of 32 channels, the ones of group m (sb(m) .. sb(m + 1) - 1,
   // at most 2) run right before main chunk m, their pixel tiles prepared during main chunk m - 1
-  const int Csc_all = p.sc_src ? p.Csc + p.Csc1 : 0, nsc = Csc_all / KT;
+  const int Csc_all = SC && p.sc_src ? p.Csc + p.Csc1 : 0, nsc = Csc_all / KT;
   auto sb = [&](int m) { return m * nsc / ncb; };
   const bool f_temb = EF < 0 ? p.temb != nullptr : (EF & EF_TEMB) != 0;
   const bool f_res = EF < 0 ? p.res != nullptr : (EF & EF_RES) != 0;
   const bool f_comb = EF < 0 ? p.comb_src != nullptr : (EF & EF_COMB) != 0;
   const bool f_stats = EF < 0 ? p.stats != nullptr : (EF & EF_STATS) != 0;
+  const bool f_nt = EF < 0 ? p.epi_nt != 0 : (EF & EF_NT) != 0;
 
   const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.wgt, p.wbytes);
   const __amdgpu_buffer_rsrc_t rws = make_rsrc(nsc ? p.sc_wgt : p.wgt, nsc ? p.sc_wbytes : p.wbytes);
@@ -158,7 +160,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
   int gc = -1;  // main chunks done by this workgroup (halo buffer parity); -1 in the prologue
   // ---- state of the group being prepared: its shortcut chunks (first pu0, count pn) and its main chunk pc
   u32x4 hv[VPT];
-  u32x4 sv[2 * SCV];
+  u32x4 sv[SC ? 2 * SCV : 1];
   float gsc[8], gsh[8];
   int pc_ch = 0;       // first channel of the main chunk
   bool pc_src1 = false;
@@ -200,6 +202,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
   };
   // shortcut vector q of the group: chunk pu0 + q / SCV, tile row (tid >> 2) + 64 (q % SCV); no transform (raw x)
   auto sc_load = [&](int q) {
+    if constexpr (!SC) return;
     // (always issued -- past the group's last shortcut chunk it re-reads its first one, a valid address -- so sv[q] is
     // defined on every path and no shortcut vector stays live across the loops)
     const int ch = (q / SCV < pn ? pu0 + q / SCV : pu0) * KT;
@@ -212,6 +215,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
     sv[q] = __builtin_amdgcn_raw_buffer_load_b128(one ? rc1 : rc0, (pix * cs + (one ? ch - p.Csc : ch) + hcol * 8) * 2, 0, 0);
   };
   auto sc_store = [&](int q) {
+    if constexpr (!SC) return;
     if (q / SCV >= pn) return;
     *(u32x4*)(smem + SCOFF + (q / SCV) * SCBYTES + swz64((tid >> 2) + 64 * (q % SCV), hcol)) = sv[q];
   };
@@ -236,11 +240,18 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
       constexpr int e0 = 2 * j, e1 = 2 * j + 1;
       if constexpr (slot == 0) { xy[e0] = a_lshl16(hv[k][j]); xy[e1] = a_andhi(hv[k][j]); }
       if constexpr (slot == 1) { a_fma(xy[e0], gsc[e0], gsh[e0]); a_fma(xy[e1], gsc[e1], gsh[e1]); }
+#ifdef H10_EXP_XF_CHEAP  // timing diagnostics only: full-rate multiplies in place of the transcendentals
+      if constexpr (slot == 2) { xe[j] = xy[j]; a_mul(xe[j], xy[j]); }
+      if constexpr (slot == 3) { xe[4 + j] = xy[4 + j]; a_mul(xe[4 + j], xy[4 + j]); }
+      if constexpr (slot == 5) a_mul(xe[j], xy[j]);
+      if constexpr (slot == 6) a_mul(xe[4 + j], xy[4 + j]);
+#else
       if constexpr (slot == 2) xe[j] = a_exp(xy[j]);
       if constexpr (slot == 3) xe[4 + j] = a_exp(xy[4 + j]);
       if constexpr (slot == 4) { a_fmamk(xe[e0], knl2); a_fmamk(xe[e1], knl2); }
       if constexpr (slot == 5) a_rcp(xe[j]);
       if constexpr (slot == 6) a_rcp(xe[4 + j]);
+#endif
       if constexpr (slot == 7) { a_mul(xy[e0], xe[e0]); a_mul(xy[e1], xe[e1]); }
       if constexpr (slot == 8) {
         xo[j] = a_cvtpk(xy[e0], xy[e1]);
@@ -282,11 +293,11 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
 #pragma unroll
   for (int k = 0; k < VPT; ++k) prep_load(k);
 #pragma unroll
-  for (int q = 0; q < 2 * SCV; ++q) sc_load(q);
+  for (int q = 0; q < (SC ? 2 * SCV : 0); ++q) sc_load(q);
 #pragma unroll
   for (int k = 0; k < VPT; ++k) prep_store(k);
 #pragma unroll
-  for (int q = 0; q < 2 * SCV; ++q) sc_store(q);
+  for (int q = 0; q < (SC ? 2 * SCV : 0); ++q) sc_store(q);
   wload(wnext, n0, pn > 0, 0, pn > 0 ? pu0 : 0);
   gc = 0;
 
@@ -371,7 +382,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
         if constexpr (st >= LOAD0 && (st - LOAD0) % STRIDE == 0 && (st - LOAD0) / STRIDE < VPT) {
           prep_load((st - LOAD0) / STRIDE);
         }
-        if constexpr (st >= SCL0 && (st - SCL0) % SCSTRIDE == 0 && (st - SCL0) / SCSTRIDE < 2 * SCV) {
+        if constexpr (SC && st >= SCL0 && (st - SCL0) % SCSTRIDE == 0 && (st - SCL0) / SCSTRIDE < 2 * SCV) {
           sc_load((st - SCL0) / SCSTRIDE);
         }
         static_for<4>([&](auto J) {
@@ -385,7 +396,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
                       (st - XF0 - NSLOT + 1) / STRIDE < VPT) {
           xf_store((st - XF0 - NSLOT + 1) / STRIDE);
         }
-        if constexpr (st >= SCL0 + SCLAG && (st - SCL0 - SCLAG) % SCSTRIDE == 0 &&
+        if constexpr (SC && st >= SCL0 + SCLAG && (st - SCL0 - SCLAG) % SCSTRIDE == 0 &&
                       (st - SCL0 - SCLAG) / SCSTRIDE < 2 * SCV) {
           sc_store((st - SCL0 - SCLAG) / SCSTRIDE);
         }
@@ -427,14 +438,19 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
       for (int e = 0; e < 2; ++e) { s1[j][e] = f32x2{0.f, 0.f}; s2[j][e] = f32x2{0.f, 0.f}; }
     const int pix0 = (bb * H + h0 + ph * 8) * W + w0 + lrow;
     const float osc = p.out_scale;
-    auto epi = [&](auto SC) {  // SC: multiply by out_scale (a uniform branch outside the element loop)
-      constexpr bool scale = decltype(SC)::value;
+    // 16-B stores: cout blocks (2 jp, 2 jp + 1) are exchanged between DPP row pairs (v_permlane16_swap), so lane
+    // (lrow, lg) stores the 8 consecutive couts n0 + chh 64 + 16 (2 jp + (lg & 1)) + 8 (lg >> 1) of its pixel -- half
+    // the store instructions of 8-B stores (the epilogue is store-issue-bound at one wave per SIMD)
+    const int cst = n0 + chh * 64 + 16 * (lg & 1) + 8 * (lg >> 1);
+    auto epi = [&](auto SC_) {  // SC_: multiply by out_scale (a uniform branch outside the element loop)
+      constexpr bool scale = decltype(SC_)::value;
       const f32x2 osc2 = f32x2{osc, osc};
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int pix = pix0 + (i >> 1) * W + (i & 1) * 16;
         f32x4 q = f32x4{0.f, 0.f, 0.f, 0.f};
         if (f_comb) q = *(const f32x4*)(p.comb_src + (size_t)pix * 4);
+        uint32_t pk[4][2];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int co = co0 + 16 * j;
@@ -458,10 +474,8 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
               v[e >> 1][e & 1] += q[0] * cw[0] + q[1] * cw[1] + q[2] * cw[2] + q[3] * cw[3] + p.comb_b[co + e];
             }
           }
-          uint2 o;
-          o.x = pack_bf16x2(v[0][0], v[0][1]);
-          o.y = pack_bf16x2(v[1][0], v[1][1]);
-          *(uint2*)((bf16_t*)p.out + (size_t)pix * p.out_ld + co) = o;
+          pk[j][0] = pack_bf16x2(v[0][0], v[0][1]);
+          pk[j][1] = pack_bf16x2(v[1][0], v[1][1]);
           if (f_stats) {
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
@@ -469,6 +483,15 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
               s2[j][e] = v[e] * v[e] + s2[j][e];
             }
           }
+        }
+        bf16_t* orow = (bf16_t*)p.out + (size_t)pix * p.out_ld + cst;
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const auto r0 = __builtin_amdgcn_permlane16_swap(pk[2 * jp][0], pk[2 * jp + 1][0], false, false);
+          const auto r1 = __builtin_amdgcn_permlane16_swap(pk[2 * jp][1], pk[2 * jp + 1][1], false, false);
+          const u32x4 o = {r0[0], r1[0], r0[1], r1[1]};
+          if (f_nt) __builtin_nontemporal_store(o, (u32x4*)(orow + 32 * jp));
+          else *(u32x4*)(orow + 32 * jp) = o;
         }
         __builtin_amdgcn_sched_barrier(0);  // one 16-px block at a time (the 256 accumulator reads are not hoisted)
       }
@@ -508,27 +531,42 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
   }
 }
 
-template <int GNM, int EF>
+template <int GNM, int EF, bool SC>
 int launch_h10_ef(const ConvParams& p, int ntiles, int grid, hipStream_t s) {
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_halo10_kernel<GNM, EF>,
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_halo10_kernel<GNM, EF, SC>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, h10::LDS);
   SNRSE_RET(attr);
-  hipLaunchKernelGGL((conv_halo10_kernel<GNM, EF>), dim3(grid), dim3(256), h10::LDS, s, p, ntiles);
+  hipLaunchKernelGGL((conv_halo10_kernel<GNM, EF, SC>), dim3(grid), dim3(256), h10::LDS, s, p, ntiles);
   return (int)hipGetLastError();
 }
 
+#define SNRSE_H10_EF(F, SC) \
+  case F: return launch_h10_ef<GNM, F, SC>(p, ntiles, grid, s);
 template <int GNM>
 int launch_h10_gn(const ConvParams& p, int ntiles, int grid, hipStream_t s, bool specialise) {
+  const bool sc = p.sc_src != nullptr;
   if (specialise && p.bias) {
-    switch (epi_flags(p) & ~EF_NT) {  // (8-byte stores: no non-temporal form)
-      case EF_TEMB | EF_STATS: return launch_h10_ef<GNM, EF_TEMB | EF_STATS>(p, ntiles, grid, s);
-      case EF_RES | EF_STATS: return launch_h10_ef<GNM, EF_RES | EF_STATS>(p, ntiles, grid, s);
-      case EF_STATS: return launch_h10_ef<GNM, EF_STATS>(p, ntiles, grid, s);
-      default: break;
+    // the NCSN++ ResBlock configurations: Conv_0 (temb), Conv_1 (residual, or the fused shortcut), non-temporal stores
+    // for outputs beyond the L2 / MALL (p.epi_nt)
+    if (!sc) {
+      switch (epi_flags(p)) {
+        SNRSE_H10_EF(EF_TEMB | EF_STATS, false)
+        SNRSE_H10_EF(EF_TEMB | EF_STATS | EF_NT, false)
+        SNRSE_H10_EF(EF_RES | EF_STATS, false)
+        SNRSE_H10_EF(EF_RES | EF_STATS | EF_NT, false)
+        default: break;
+      }
+    } else {
+      switch (epi_flags(p)) {
+        SNRSE_H10_EF(EF_STATS, true)
+        SNRSE_H10_EF(EF_STATS | EF_NT, true)
+        default: break;
+      }
     }
   }
-  return launch_h10_ef<GNM, EF_RT>(p, ntiles, grid, s);
+  return sc ? launch_h10_ef<GNM, EF_RT, true>(p, ntiles, grid, s) : launch_h10_ef<GNM, EF_RT, false>(p, ntiles, grid, s);
 }
+#undef SNRSE_H10_EF
 
 }  // namespace
 

@@ -122,3 +122,23 @@ def test_h10_repeat_is_deterministic_and_stats_accumulate_once(gpu):
     o2, s2, _ = run(10)
     assert torch.equal(o1, o2)
     assert rel(ops.fold_stats(s1), ops.fold_stats(s2)) < 1e-12
+
+
+@pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[8]])
+def test_h10_nontemporal_epilogue_matches(gpu, case):
+    """The non-temporal form of the 16-B epilogue stores (option epi_nt = 1, which the auto mode takes for outputs
+    beyond 256 MB, e.g. every level-0 conv at C2) writes the same bytes as the cached form."""
+    from snrse import ops
+    _, run = _case(gpu, case)
+    outs = []
+    for nt in (1, 0):
+        ops.set_option("epi_nt", nt)
+        try:
+            o, st, ran = run(10)
+            assert ran == "conv_halo10_kernel" and ops.get_option("last_epi_nt") == nt
+        finally:
+            ops.set_option("epi_nt", 2)
+        outs.append((o, st))
+    assert torch.equal(outs[0][0], outs[1][0])
+    if outs[0][1] is not None:
+        assert rel(ops.fold_stats(outs[0][1]), ops.fold_stats(outs[1][1])) < 1e-12

@@ -9,8 +9,9 @@ cd /tmp && export TMPDIR=/tmp
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
 P2="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAVES"
 P3="SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA SQ_CYCLES SQ_INSTS_BRANCH"
+P4="GRBM_GUI_ACTIVE GRBM_COUNT"
 i=0
-for P in "$P1" "$P2" "$P3"; do
+for P in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d "$OUT/pass$i" -o run -- \
     python3 "$ROOT/tools/conv_bench.py" --variants "$V" --shapes "$S" --reps 2 --rounds 1 --gn > "$OUT/pass$i.log" 2>&1
