@@ -101,6 +101,14 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
   const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
   const int t_begin = (int)((long long)g * ntiles / nb), t_end = (int)((long long)(g + 1) * ntiles / nb);
   if (t_begin >= t_end) return;
+#ifdef H10_STAGGER  // experiment: workgroups start in 4 phases H10_STAGGER x 10 ns apart, so their epilogues (which write
+                    // 128 KB each) do not all fall in the same interval
+  {
+    const long long t0 = __builtin_amdgcn_s_memrealtime();
+    const long long dt = (long long)(bid & 3) * H10_STAGGER;
+    while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
+  }
+#endif
 
   const int H = p.H, W = p.W;
   const int ntw = W / TW, nth = H / TH;
