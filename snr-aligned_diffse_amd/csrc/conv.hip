@@ -1783,8 +1783,11 @@ int dispatch_conv(const ConvParams& p, hipStream_t s, snrse_ctx& cx) {
         // H % 8 == 0.  Not on W = 32 (level 4): 128 tiles for 512 workgroup slots ran 11-45 % slower there
         // than the split-K LDS-DMA GEMM + gn_act (profiles/r03v_level4_halo_vs_glds.jsonl)
         if constexpr (sizeof(TO) == 2) {
-          // v10 (conv_h10.hip): forced by conv_variant 10, taken by variant 0 under option h10 on v5's shapes
-          if ((cx.conv_variant == 10 || (cx.conv_variant == 0 && cx.h10 && halo_tile64(p))) && h10_ok(p)) {
+          // v10 (conv_h10.hip): forced by conv_variant 10; taken by variant 0 on v5's shapes under option h10 = 1, and under
+          // h10 = 2 for the concatenated-input convs without a shortcut (the up path's Conv_0, where it measured ~4 %
+          // faster than v5: 8 chunks per tile amortise its epilogue; profiles/r04_v10_ablations.jsonl)
+          const bool h10_auto = cx.conv_variant == 0 && halo_tile64(p) && (cx.h10 == 1 || (cx.h10 == 2 && p.C1 > 0 && !p.sc_src));
+          if ((cx.conv_variant == 10 || h10_auto) && h10_ok(p)) {
             if (!cx.num_cu) {
               int dev = 0;
               SNRSE_RET(hipGetDevice(&dev));
@@ -1888,7 +1891,7 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
     if (x3) {
       const int x3h_tiles = q.B * (q.H / x3h::TH) * ((q.W + x3h::TW - 1) / x3h::TW) * (q.Cout / 128);
       // the v10 structure's split-bf16 form (option h10) on the x3h kernel's shapes where its 8 x 32 tiles fit
-      if (cx.h10 && x3h_all && h10x3_ok(q)) {
+      if (cx.h10 == 1 && x3h_all && h10x3_ok(q)) {
         if (!cx.num_cu) {
           int dev = 0;
           SNRSE_RET(hipGetDevice(&dev));

@@ -443,6 +443,9 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
     // the asm MFMAs' results are read by the epilogue's v_accvgpr_read: wait states hipcc does not insert
     asm volatile("s_nop 15\n\ts_nop 15" ::: "memory");
 
+#ifdef H10_EXP_NOEPI2  // timing diagnostics: the epilogue exists but is skipped at run time (out_scale never equals this)
+    if (p.out_scale != 12345.f) continue;
+#endif
 #ifdef H10_EXP_NOEPI
     {
       float* o = (float*)p.out + (size_t)t * 256 * 64 + lane * 4;
