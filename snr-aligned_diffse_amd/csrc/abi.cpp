@@ -74,7 +74,8 @@ int set_option(snrse_ctx& c, const char* name, int value) {
 int get_option(const snrse_ctx& c, const char* name, int* value) {
   if (!name || !value) return SNRSE_EINVAL;
   if (const int* f = option_field(const_cast<snrse_ctx&>(c), name)) { *value = *f; return 0; }
-  if (name_is(name, "halo_kernel")) { *value = c.h10 ? 12 : 5; return 0; }  // the halo generation variant 0 takes
+  if (name_is(name, "halo_kernel")) { *value = c.h10 == 1 ? 12 : 5; return 0; }  // the halo generation variant 0 takes
+  // for a single-input conv (under h10 = 2 the concatenated-input ones without a shortcut take 12)
   if (name_is(name, "last_kernel")) { *value = c.last_kernel; return 0; }
   if (name_is(name, "last_ksplit")) { *value = c.last_ksplit; return 0; }
   if (name_is(name, "last_epi_nt")) { *value = c.last_epi_nt; return 0; }

@@ -78,6 +78,8 @@ def test_h10x3_vs_f64_and_x3h(gpu, case):
             kw["comb_b"].double()[:, None, None]
     wp = ops.split_weight(w.reshape(Co, -1))
 
+    h10_prev = ops.get_option("h10")
+
     def run(h10):
         st = ops.new_stats(B, Co) if use_st else None
         ops.set_option("h10", h10)
@@ -86,7 +88,7 @@ def test_h10x3_vs_f64_and_x3h(gpu, case):
             out = ops.conv2d(x0, wp, 3, Co, bias=bias, src1=x1, stats=st, gn=gn, gn_act=gnm == 2, **kw)
             ran = ops.kernel_name(ops.get_option("last_kernel"))
         finally:
-            ops.set_option("h10", 0)
+            ops.set_option("h10", h10_prev)
             ops.set_option("x3_tile", 0)
         return out, st, ran
 
