@@ -155,9 +155,10 @@ def pc_vs_golden(dev, net=None, dtype=torch.bfloat16):
 # 24-36 dB with a median of 32 dB, except where a clip's trajectory amplifies the bf16 rounding -- one clip of the
 # bench batch at 11 dB (rel RMS 0.27); the same clip under other Philox draws (the batch rolled by 5) agrees at 35 dB
 # and no position is systematically off, so it is a property of that (clip, noise) trajectory through 60 NFEs of a
-# formula-weight network, not of a batch slot.  Bounds: median >= 28 dB, >= 90 % of the clips >= 25 dB, every clip
-# >= 10 dB (finite), mean relative RMS <= 5e-2.
-C2_AGREE = {"si_sdr_median_min_db": 28.0, "frac_ge_25db_min": 0.9, "si_sdr_min_db": 10.0, "rel_rms_mean_max": 5e-2}
+# formula-weight network, not of a batch slot (with the v10 kernel on the concatenated-input convs -- another fp32
+# summation order -- the same clip measured 10.5 dB, profiles/r04j_bench_line.json).  Bounds: median >= 28 dB, >= 90 %
+# of the clips >= 25 dB, mean relative RMS <= 5e-2, and every clip >= 5 dB (no trajectory diverges outright).
+C2_AGREE = {"si_sdr_median_min_db": 28.0, "frac_ge_25db_min": 0.9, "si_sdr_min_db": 5.0, "rel_rms_mean_max": 5e-2}
 
 
 def waveform_agreement(est, ref, per_clip=False):

@@ -300,6 +300,131 @@ __global__ __launch_bounds__(256) void input_conv_kernel(const float2* __restric
   unsafeAtomicAdd(&stats[stat_idx(b, slot, tid >> 1, 128) + (tid & 1)], (double)tot);
 }
 
+// ---- the same input conv with the workgroup's input rows staged in LDS (W <= 1024) ----------------------------
+// A workgroup's 16 tiles (1024 consecutive pixels of one image) read their 3x3 neighbours from the image rows they
+// span plus one above and below, loaded into LDS in one burst at the start (16 B per pixel: x.re, x.im, y.re, y.im),
+// so the per-block neighbour loads of input_conv_kernel -- one block of prefetch, an HBM latency exposed per 16-px
+// block -- become LDS reads, and the launch is bound by its 256 B/pixel of output stores.  Same MFMA / epilogue /
+// statistics as input_conv_kernel.
+__global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __restrict__ x, const float2* __restrict__ y,
+                                                             int H, int W, const bf16_t* __restrict__ wgt,
+                                                             const float* __restrict__ bias, bf16_t* __restrict__ out,
+                                                             float* __restrict__ pyr, double* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) char ic_smem[];
+  __shared__ float s_st[4][128 * 2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, lr = lane & 15;
+  const int HW = H * W, tpr = W / 64;
+  const long long p0 = (long long)blockIdx.x * 1024;  // first pixel of the workgroup (16 tiles x 64 px)
+  const int b = (int)(p0 / HW);
+  const size_t img = (size_t)b * HW;
+  const int q0 = (int)(p0 - (long long)b * HW);
+  const int r0 = q0 / W - 1, nrows = (q0 + 1023) / W + 2 - r0;  // staged image rows r0 .. r0 + nrows - 1
+  // ---- stage: pixel pairs (2 x float4 loads -> 2 x 16-B LDS rows), rows outside the image zero
+  float4* st = (float4*)ic_smem;
+  const int npair = nrows * W / 2;
+  for (int i = tid; i < npair; i += 256) {
+    const int rr = (2 * i) / W, cc = 2 * i - rr * W, ih = r0 + rr;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
+    if ((unsigned)ih < (unsigned)H) {
+      a = *(const float4*)(x + img + (size_t)ih * W + cc);
+      c = *(const float4*)(y + img + (size_t)ih * W + cc);
+    }
+    st[2 * i] = make_float4(a.x, a.y, c.x, c.y);
+    st[2 * i + 1] = make_float4(a.z, a.w, c.z, c.w);
+  }
+  u32x4 wf[8][2];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) wf[j][s] = *(const u32x4*)(wgt + (16 * j + lr) * 64 + 32 * s + 8 * g);
+  float bv[8][4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const f32x4 b4 = *(const f32x4*)(bias + 16 * j + 4 * g);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bv[j][e] = b4[e];
+  }
+  float s1[8][4], s2[8][4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { s1[j][e] = 0.f; s2[j][e] = 0.f; }
+  int tdy[3], tdx[3];
+  bool tuse[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int tap = u < 2 ? 2 * g + u : 8;
+    tuse[u] = u < 2 || g == 0;
+    tdy[u] = tap / 3 - 1;
+    tdx[u] = tap % 3 - 1;
+  }
+  __syncthreads();
+  const int tile0 = q0 / 64 + wid * IC_TPW;  // this wave's first 64-px tile within the image
+  for (int q = 0; q < 4 * IC_TPW; ++q) {
+    const int tile = tile0 + (q >> 2);
+    const int h = tile / tpr, w = (tile - h * tpr) * 64 + 16 * (q & 3) + lr;
+    float4 v[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int hh = h + tdy[u], ww = w + tdx[u];
+      const bool ok = tuse[u] && (unsigned)ww < (unsigned)W;  // (rows: staged, zero outside the image)
+      const float4 t = st[(hh - r0) * W + (ok ? ww : w)];
+      v[u] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    u32x4 pf[2];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int sl = u < 2 ? 0 : 1, hw_ = u < 2 ? 2 * u : 0;
+      pf[sl][hw_] = pack_bf16x2(v[u].x, v[u].y);
+      pf[sl][hw_ + 1] = pack_bf16x2(v[u].z, v[u].w);
+    }
+    pf[1][2] = 0u;
+    pf[1][3] = 0u;
+    if (g == 2)  // tap 4 = the pixel itself: the input pyramid
+      *(float4*)(pyr + (img + (size_t)h * W + w) * 4) = v[0];
+    bf16_t* orow = out + (img + (size_t)h * W + w) * 128 + 8 * (g >> 1);
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) {
+      uint32_t pk[2][2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int j = 2 * jp + hh;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc = mfma_bf16_16x16x32(wf[j][0], pf[0], acc);
+        acc = mfma_bf16_16x16x32(wf[j][1], pf[1], acc);
+        float vv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          vv[e] = acc[e] + bv[j][e];
+          s1[j][e] += vv[e];
+          s2[j][e] = fmaf(vv[e], vv[e], s2[j][e]);
+        }
+        pk[hh][0] = pack_bf16x2(vv[0], vv[1]);
+        pk[hh][1] = pack_bf16x2(vv[2], vv[3]);
+      }
+      const auto a0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+      const auto a1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+      const u32x4 o = {a0[0], a1[0], a0[1], a1[1]};
+      *(u32x4*)(orow + 16 * (2 * jp + (g & 1))) = o;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a = ic_row_sum16(s1[j][e]), qq = ic_row_sum16(s2[j][e]);
+      if (lr == 0) {
+        s_st[wid][(16 * j + 4 * g + e) * 2] = a;
+        s_st[wid][(16 * j + 4 * g + e) * 2 + 1] = qq;
+      }
+    }
+  __syncthreads();
+  const int slot = blockIdx.x & (SNRSE_STAT_SLOTS - 1);
+  const float tot = (s_st[0][tid] + s_st[1][tid]) + (s_st[2][tid] + s_st[3][tid]);
+  unsafeAtomicAdd(&stats[stat_idx(b, slot, tid >> 1, 128) + (tid & 1)], (double)tot);
+}
+
 // ---- Philox4x32-10 -> Box-Muller complex normals -------------------------------------
 SNRSE_DEV uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t& hi) {
   const uint64_t p = (uint64_t)a * b;
@@ -450,6 +575,17 @@ extern "C" int snrse_input_conv(snrse_ctx* ctx, const void* x, const void* y, in
   if (!snrse_ctx_resolve(ctx)->stats_zeroed)
     SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * 128, s));
   const long long blocks = (long long)B * H * W / (64 * 16);
+  // LDS-staged form: the rows 1024 pixels span + 2 halo rows, <= (1023 / W + 4) * W * 16 B (64 KB at W = 1024)
+  const int lds_rows = 1023 / W + 4;  // (a 1024-px range can touch 1023 / W + 2 rows when W does not divide 1024)
+  if (W <= 1024 && snrse_ctx_resolve(ctx)->ic_lds) {
+    const size_t lds = (size_t)lds_rows * W * 16;
+    static const hipError_t attr = hipFuncSetAttribute((const void*)input_conv_lds_kernel,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+    SNRSE_RET(attr);
+    hipLaunchKernelGGL(input_conv_lds_kernel, dim3((unsigned)blocks), dim3(256), lds, s, (const float2*)x,
+                       (const float2*)y, H, W, (const bf16_t*)wgt, bias, (bf16_t*)out, pyr, stats);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(input_conv_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const float2*)x, (const float2*)y,
                      H, W, (const bf16_t*)wgt, bias, (bf16_t*)out, pyr, stats);
   return (int)hipGetLastError();

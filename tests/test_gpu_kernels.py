@@ -691,6 +691,31 @@ def test_input_conv_fused_vs_im2col_gemm(gpu):
     assert not ops.input_conv_ok(ok_shape)  # 8 x 64 px = 8 tiles: outside the contract
 
 
+@pytest.mark.parametrize("shape", [(2, 256, 128), (1, 16, 64), (1, 256, 384), (1, 64, 1024), (2, 32, 512), (1, 48, 320)])
+def test_input_conv_lds_staged_matches_streaming(gpu, shape):
+    """The LDS-staged input conv (option ic_lds, W <= 1024: the workgroup's rows + 2 halo rows loaded once) writes the
+    same h and pyramid bytes as the streaming form and the same statistics, including widths that do not divide the
+    workgroup's 1024 pixels (W = 384, 320: a workgroup spans partial rows) and the first / last image rows."""
+    from snrse import ops
+    B, F, T = shape
+    g = torch.Generator().manual_seed(F + T)
+    x = torch.complex(torch.randn(B, F, T, generator=g), torch.randn(B, F, T, generator=g)).to(gpu)
+    y = torch.complex(torch.randn(B, F, T, generator=g), torch.randn(B, F, T, generator=g)).to(gpu)
+    wp = torch.cat([torch.randn(128, 36, generator=g) / 6, torch.zeros(128, 28)], 1).bfloat16().to(gpu).contiguous()
+    bias = (torch.randn(128, generator=g) * 0.1).to(gpu)
+    assert ops.input_conv_ok(x)
+    outs = []
+    for v in (1, 0):
+        ops.set_option("ic_lds", v)
+        try:
+            outs.append(ops.input_conv(x, y, wp, bias))
+        finally:
+            ops.set_option("ic_lds", 1)
+    (h1, s1, p1), (h0, s0, p0) = outs
+    assert torch.equal(h1, h0) and torch.equal(p1, p0)
+    assert torch.allclose(s1.sum(1), s0.sum(1), rtol=1e-9, atol=1e-9)
+
+
 @pytest.mark.parametrize("shape", [(2, 128, 8, 16), (1, 256, 36, 70), (3, 16, 18, 34), (2, 128, 64, 256),
                                    (1, 512, 6, 40), (2, 8, 8, 8), (1, 64, 20, 12)])
 def test_gn_resample_down_rows(gpu, shape):
