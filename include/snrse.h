@@ -160,12 +160,18 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  *   4 x 64 px x 128 couts, any W, else register-staged 128 x 128), register-staged tiles 1 128 px x 128 couts,
  *   2 256 x 128, 3 128 x 256 (Cout % 256 == 0), 4 the halo kernel wherever its shape conditions hold;
  * "stats_zeroed" 1 = the statistics buffers handed to snrse_conv2d / snrse_gn_stats are already zero (the
- * caller clears one arena per network evaluation), so they skip their per-call memset. */
+ * caller clears one arena per network evaluation), so they skip their per-call memset;
+ * "h10" the v10 halo GEMM under conv_variant 0 (conv_variant 10 forces it): 2 (default) the concatenated-input
+ *   3x3 convs without a shortcut, 1 every conv the v5 halo GEMM would take (and its split-bf16 form in the
+ *   fp32x3 mode), 0 off;
+ * "ic_lds" 1 (default) the bf16 input conv stages its workgroup's input rows in LDS (W <= 1024), 0 the
+ *   streaming form (bit-identical). */
 int snrse_set_option(const char* name, int value);
 
 /* Read back a switch (any name above) or: "halo_kernel" = generation of the halo conv kernel the current
- * setting dispatches to (5), "last_kernel" = generation of the most recent snrse_conv2d launch (1 v1, 2 v2,
- * 3 / 4 split-bf16 register-staged / halo, 5 halo, 10 pyramid head, 11 split-bf16 pyramid head), "last_ksplit" = K splits of the most recent v2 launch, "last_epi_nt" /
+ * setting dispatches a single-input conv to (5, or 12 under h10 = 1), "last_kernel" = generation of the most recent snrse_conv2d launch (1 v1, 2 v2,
+ * 3 / 4 split-bf16 register-staged / halo, 5 halo, 10 pyramid head, 11 split-bf16 pyramid head, 12 v10 halo,
+ * 13 split-bf16 v10 halo), "last_ksplit" = K splits of the most recent v2 launch, "last_epi_nt" /
  * "last_chunks" = store flavour / image-range launches of the most recent halo conv, "last_tw" = its tile
  * width (32 / 64). */
 int snrse_get_option(const char* name, int* value);
