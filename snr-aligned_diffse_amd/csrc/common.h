@@ -102,7 +102,8 @@ struct snrse_ctx {
   int resample_down_rows = 4;  // output rows per down-sampling row strip (1, 2, 4; 4 fastest since r03)
   int x3_tile = 0;             // split-bf16 fp32 GEMM tile: 0 auto, 1 128x128, 2 256x128, 3 128x256, 4 halo
   int x3_spread = 1;           // halo split GEMM: next chunk's halo stored one piece per tap (0: in one go)
-  int ic_lds = 1;              // bf16 input conv with the workgroup's input rows staged in LDS (W <= 1024)
+  int ic_lds = 1;              // bf16 input conv: 1 the workgroup's input rows staged in LDS (W <= 1024), 2 the same
+                               // with the channels split over wave pairs (4 waves / SIMD), 0 streaming loads
   int h10 = 2;                 // v10 halo GEMM under conv_variant 0: 1 = every bf16 3x3 conv v5 takes (and v10x3 in
                                // fp32x3), 2 = the concatenated-input ones without a shortcut, 0 = off
   int num_cu = 0;              // compute units of the device (v10 persistent grid), read on first use

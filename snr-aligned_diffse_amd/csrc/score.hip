@@ -306,14 +306,21 @@ __global__ __launch_bounds__(256) void input_conv_kernel(const float2* __restric
 // so the per-block neighbour loads of input_conv_kernel -- one block of prefetch, an HBM latency exposed per 16-px
 // block -- become LDS reads, and the launch is bound by its 256 B/pixel of output stores.  Same MFMA / epilogue /
 // statistics as input_conv_kernel.
+// ICH: output channels per wave (128: a wave owns 4 of the workgroup's 16 tiles; 64: waves (2 s, 2 s + 1) share pixel
+// stream s = 8 tiles and split the channels -- half the weight / bias / statistics registers, so more waves per SIMD
+// hide the store and LDS latency)
+template <int ICH>
 __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __restrict__ x, const float2* __restrict__ y,
                                                              int H, int W, const bf16_t* __restrict__ wgt,
                                                              const float* __restrict__ bias, bf16_t* __restrict__ out,
                                                              float* __restrict__ pyr, double* __restrict__ stats) {
+  constexpr int NJ = ICH / 16, NS = 128 / ICH;  // channel blocks per wave; waves per pixel stream
+  constexpr int TPS = 16 / (4 / NS);            // tiles per pixel stream (4 with ICH 128, 8 with 64)
   extern __shared__ __attribute__((aligned(16))) char ic_smem[];
   __shared__ float s_st[4][128 * 2];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, lr = lane & 15;
+  const int ps = wid / NS, jb = (wid % NS) * NJ;  // pixel stream, first channel block of this wave
   const int HW = H * W, tpr = W / 64;
   const long long p0 = (long long)blockIdx.x * 1024;  // first pixel of the workgroup (16 tiles x 64 px)
   const int b = (int)(p0 / HW);
@@ -333,21 +340,21 @@ __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __res
     st[2 * i] = make_float4(a.x, a.y, c.x, c.y);
     st[2 * i + 1] = make_float4(a.z, a.w, c.z, c.w);
   }
-  u32x4 wf[8][2];
+  u32x4 wf[NJ][2];
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) wf[j][s] = *(const u32x4*)(wgt + (16 * j + lr) * 64 + 32 * s + 8 * g);
-  float bv[8][4];
+    for (int s = 0; s < 2; ++s) wf[j][s] = *(const u32x4*)(wgt + (16 * (jb + j) + lr) * 64 + 32 * s + 8 * g);
+  float bv[NJ][4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const f32x4 b4 = *(const f32x4*)(bias + 16 * j + 4 * g);
+  for (int j = 0; j < NJ; ++j) {
+    const f32x4 b4 = *(const f32x4*)(bias + 16 * (jb + j) + 4 * g);
 #pragma unroll
     for (int e = 0; e < 4; ++e) bv[j][e] = b4[e];
   }
-  float s1[8][4], s2[8][4];
+  float s1[NJ][4], s2[NJ][4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) { s1[j][e] = 0.f; s2[j][e] = 0.f; }
   int tdy[3], tdx[3];
@@ -360,8 +367,8 @@ __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __res
     tdx[u] = tap % 3 - 1;
   }
   __syncthreads();
-  const int tile0 = q0 / 64 + wid * IC_TPW;  // this wave's first 64-px tile within the image
-  for (int q = 0; q < 4 * IC_TPW; ++q) {
+  const int tile0 = q0 / 64 + ps * TPS;  // this pixel stream's first 64-px tile within the image
+  for (int q = 0; q < 4 * TPS; ++q) {
     const int tile = tile0 + (q >> 2);
     const int h = tile / tpr, w = (tile - h * tpr) * 64 + 16 * (q & 3) + lr;
     float4 v[3];
@@ -381,11 +388,11 @@ __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __res
     }
     pf[1][2] = 0u;
     pf[1][3] = 0u;
-    if (g == 2)  // tap 4 = the pixel itself: the input pyramid
+    if (g == 2 && jb == 0)  // tap 4 = the pixel itself: the input pyramid (written by one wave of the stream)
       *(float4*)(pyr + (img + (size_t)h * W + w) * 4) = v[0];
     bf16_t* orow = out + (img + (size_t)h * W + w) * 128 + 8 * (g >> 1);
 #pragma unroll
-    for (int jp = 0; jp < 4; ++jp) {
+    for (int jp = 0; jp < NJ / 2; ++jp) {
       uint32_t pk[2][2];
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
@@ -406,22 +413,27 @@ __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __res
       const auto a0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
       const auto a1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
       const u32x4 o = {a0[0], a1[0], a0[1], a1[1]};
-      *(u32x4*)(orow + 16 * (2 * jp + (g & 1))) = o;
+      *(u32x4*)(orow + 16 * (jb + 2 * jp + (g & 1))) = o;
     }
   }
+  // statistics: s_st[pixel stream][channel][2] (each channel written by one wave per stream), then a fixed-order
+  // fold over the 4 / NS streams
 #pragma unroll
-  for (int j = 0; j < 8; ++j)
+  for (int j = 0; j < NJ; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float a = ic_row_sum16(s1[j][e]), qq = ic_row_sum16(s2[j][e]);
       if (lr == 0) {
-        s_st[wid][(16 * j + 4 * g + e) * 2] = a;
-        s_st[wid][(16 * j + 4 * g + e) * 2 + 1] = qq;
+        s_st[ps][(16 * (jb + j) + 4 * g + e) * 2] = a;
+        s_st[ps][(16 * (jb + j) + 4 * g + e) * 2 + 1] = qq;
       }
     }
   __syncthreads();
   const int slot = blockIdx.x & (SNRSE_STAT_SLOTS - 1);
-  const float tot = (s_st[0][tid] + s_st[1][tid]) + (s_st[2][tid] + s_st[3][tid]);
+  float tot = s_st[0][tid];
+#pragma unroll
+  for (int k = 1; k < 4 / NS; ++k) tot += s_st[k][tid];
+  if (NS == 1) tot = (s_st[0][tid] + s_st[1][tid]) + (s_st[2][tid] + s_st[3][tid]);  // (the streaming kernel's order)
   unsafeAtomicAdd(&stats[stat_idx(b, slot, tid >> 1, 128) + (tid & 1)], (double)tot);
 }
 
@@ -579,11 +591,18 @@ extern "C" int snrse_input_conv(snrse_ctx* ctx, const void* x, const void* y, in
   const int lds_rows = 1023 / W + 4;  // (a 1024-px range can touch 1023 / W + 2 rows when W does not divide 1024)
   if (W <= 1024 && snrse_ctx_resolve(ctx)->ic_lds) {
     const size_t lds = (size_t)lds_rows * W * 16;
-    static const hipError_t attr = hipFuncSetAttribute((const void*)input_conv_lds_kernel,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
-    SNRSE_RET(attr);
-    hipLaunchKernelGGL(input_conv_lds_kernel, dim3((unsigned)blocks), dim3(256), lds, s, (const float2*)x,
-                       (const float2*)y, H, W, (const bf16_t*)wgt, bias, (bf16_t*)out, pyr, stats);
+    static const hipError_t attr1 = hipFuncSetAttribute((const void*)input_conv_lds_kernel<128>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+    static const hipError_t attr2 = hipFuncSetAttribute((const void*)input_conv_lds_kernel<64>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+    SNRSE_RET(attr1);
+    SNRSE_RET(attr2);
+    if (snrse_ctx_resolve(ctx)->ic_lds == 2)
+      hipLaunchKernelGGL(input_conv_lds_kernel<64>, dim3((unsigned)blocks), dim3(256), lds, s, (const float2*)x,
+                         (const float2*)y, H, W, (const bf16_t*)wgt, bias, (bf16_t*)out, pyr, stats);
+    else
+      hipLaunchKernelGGL(input_conv_lds_kernel<128>, dim3((unsigned)blocks), dim3(256), lds, s, (const float2*)x,
+                         (const float2*)y, H, W, (const bf16_t*)wgt, bias, (bf16_t*)out, pyr, stats);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(input_conv_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const float2*)x, (const float2*)y,

@@ -691,11 +691,13 @@ def test_input_conv_fused_vs_im2col_gemm(gpu):
     assert not ops.input_conv_ok(ok_shape)  # 8 x 64 px = 8 tiles: outside the contract
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("shape", [(2, 256, 128), (1, 16, 64), (1, 256, 384), (1, 64, 1024), (2, 32, 512), (1, 48, 320)])
-def test_input_conv_lds_staged_matches_streaming(gpu, shape):
-    """The LDS-staged input conv (option ic_lds, W <= 1024: the workgroup's rows + 2 halo rows loaded once) writes the
-    same h and pyramid bytes as the streaming form and the same statistics, including widths that do not divide the
-    workgroup's 1024 pixels (W = 384, 320: a workgroup spans partial rows) and the first / last image rows."""
+def test_input_conv_lds_staged_matches_streaming(gpu, shape, mode):
+    """The LDS-staged input conv (option ic_lds 1, or 2 with the channels split over wave pairs; W <= 1024: the
+    workgroup's rows + 2 halo rows loaded once) writes the same h and pyramid bytes as the streaming form and the same
+    statistics (mode 2 folds its f32 partial sums over other pixel groups: to 1e-5), including widths that do not
+    divide the workgroup's 1024 pixels (W = 384, 320: a workgroup spans partial rows) and the first / last rows."""
     from snrse import ops
     B, F, T = shape
     g = torch.Generator().manual_seed(F + T)
@@ -705,7 +707,7 @@ def test_input_conv_lds_staged_matches_streaming(gpu, shape):
     bias = (torch.randn(128, generator=g) * 0.1).to(gpu)
     assert ops.input_conv_ok(x)
     outs = []
-    for v in (1, 0):
+    for v in (mode, 0):
         ops.set_option("ic_lds", v)
         try:
             outs.append(ops.input_conv(x, y, wp, bias))
@@ -713,7 +715,8 @@ def test_input_conv_lds_staged_matches_streaming(gpu, shape):
             ops.set_option("ic_lds", 1)
     (h1, s1, p1), (h0, s0, p0) = outs
     assert torch.equal(h1, h0) and torch.equal(p1, p0)
-    assert torch.allclose(s1.sum(1), s0.sum(1), rtol=1e-9, atol=1e-9)
+    tol = 1e-9 if mode == 1 else 1e-5
+    assert torch.allclose(s1.sum(1), s0.sum(1), rtol=tol, atol=tol * float(s0.sum(1).abs().max()))
 
 
 @pytest.mark.parametrize("shape", [(2, 128, 8, 16), (1, 256, 36, 70), (3, 16, 18, 34), (2, 128, 64, 256),

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""A/B of the bf16 input conv forms (option ic_lds: 1 = input rows staged in LDS, 0 = streaming neighbour loads) on
+"""A/B of the bf16 input conv forms (option ic_lds: 1 = input rows staged in LDS, 2 = the same with the channels split over wave pairs,
+0 = streaming neighbour loads) on
 the C2 shape [32, 256, 512] (HIP events on the launch stream, interleaved).  HBM bytes per launch: 16 B read + 256 B
 (h) + 16 B (pyramid) written per pixel.  Usage: python tools/ic_bench.py [--reps 20] [--rounds 3]"""
 import argparse
@@ -30,7 +31,7 @@ def main():
     bias = torch.randn(128, device=dev, generator=g) * 0.1
     nbytes = B * F * T * (16 + 256 + 16)
     for r in range(a.rounds):
-        for v in (0, 1):
+        for v in (0, 1, 2):
             ops.set_option("ic_lds", v)
             ops.input_conv(x, y, wp, bias)
             s = torch.cuda.current_stream()
