@@ -54,8 +54,11 @@ SNRSE_DEV int kh_swz(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >
   } while (0)
 
 // grid: B * (H / 4) * (W / 64) workgroups of 256.  GNM: 0 no prologue, 1 GroupNorm affine, 2 + SiLU
+#ifndef SNRSE_HEAD_MINB
+#define SNRSE_HEAD_MINB 1  // workgroups per CU the register allocation is bounded for (A/B builds)
+#endif
 template <int GNM>
-__global__ __launch_bounds__(256) void conv_head_kernel(ConvParams p) {
+__global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvParams p) {
   __shared__ __attribute__((aligned(16))) char smem[KH_LDS];
   char* const halo = smem;
   char* const wsl = smem + KH_HALO;
