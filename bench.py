@@ -549,7 +549,9 @@ def run(args):
         fl, ms, n = by[kname]
         ach = fl / (ms * 1e-3) if ms > 0 else 0.0
         peak = PEAK[args.dtype]
-        traffic, tsrc = pmc_traffic(kname.split("+")[0], args.config)  # (a family: its first kernel's launches)
+        traffic, tsrc = pmc_traffic(kname, args.config)
+        if traffic is None and "+" in kname:  # no family profile: its first kernel's launches
+            traffic, tsrc = pmc_traffic(kname.split("+")[0], args.config)
         roof = {"bound": "mfma", "achieved": ach / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
                 "frac": ach / peak, "traffic": traffic, "kernel": kname, "launches_per_pass": n,
                 "avg_launch_us": ms * 1e3 / max(n, 1), "flop_per_launch": fl / max(n, 1),
