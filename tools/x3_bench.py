@@ -63,10 +63,11 @@ def main():
         if args.h10:
             variants = [("x3gn10" if args.gn else "x310", 0, 1)] + variants
         ref = None
+        h10_prev = ops.get_option("h10")
         for kind, t, sp in variants:
             ops.set_option("x3_tile", t)
             ops.set_option("x3_spread", sp)
-            ops.set_option("h10", 1 if kind.endswith("10") else 0)
+            ops.set_option("h10", 1 if kind.endswith("10") else 0)  # (x3 takes v10x3 only under h10 = 1)
             wt = w if kind == "exact" else ws
             kw = {"gn": gn} if kind.startswith("x3gn") else {}
             fn = lambda: ops.conv2d(x0, wt, 3, Co, bias=b, src1=x1, out=out, stats=st, **kw)  # noqa: E731
@@ -82,7 +83,7 @@ def main():
                               "ksplit": ops.get_option("last_ksplit"), "rel_vs_first": err}), flush=True)
         ops.set_option("x3_tile", 0)
         ops.set_option("x3_spread", 1)
-        ops.set_option("h10", 0)
+        ops.set_option("h10", h10_prev)
         del x0, x1, out, ref
 
 
