@@ -137,7 +137,10 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] = __float_as_uint(v[k]);
     }
-    *(u32x4*)((TO*)p.out + (size_t)m * p.out_ld + n) = o;
+    if (p.epi_nt)  // (the fp32x3 halo GEMM under option x3_nt; 0 on every other launch through here)
+      __builtin_nontemporal_store(o, (u32x4*)((TO*)p.out + (size_t)m * p.out_ld + n));
+    else
+      *(u32x4*)((TO*)p.out + (size_t)m * p.out_ld + n) = o;
     if (p.stats) {
       if (one_b) {
 #pragma unroll
@@ -1904,7 +1907,13 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
       if (x3h_all) {
         cx.last_kernel = 4;
         cx.last_ksplit = 1;
-        return launch_x3h(q, stream, x3h_tiles, cx.x3_spread);
+        // non-temporal output stores as the bf16 halo GEMMs decide them (option x3_nt: the f32 outputs of the
+        // level-0 / level-1 convs are 0.5-2 GB, far beyond the Infinity Cache)
+        ConvParams r = q;
+        r.epi_nt = cx.x3_nt && (cx.epi_nt == 2 ? ((long long)q.M * q.out_ld * 4ll > ((long long)cx.epi_nt_mb << 20))
+                                               : cx.epi_nt != 0);
+        cx.last_epi_nt = r.epi_nt;
+        return launch_x3h(r, stream, x3h_tiles, cx.x3_spread);
       }
       if (q.Cout <= 16 && cx.conv_variant != 1 && head_ok(q)) {  // the pyramid heads, GroupNorm fused
         cx.last_kernel = 11;

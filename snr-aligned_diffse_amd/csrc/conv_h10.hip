@@ -337,8 +337,10 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
       for (int u = sb(c); u < u_end; ++u) {
         const int sbuf = u - sb(c);
         const bool nxt_sc = u + 1 < u_end;  // the next chunk: shortcut u + 1, else main chunk c (tap 0)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        if (sbuf == 0) {  // both shortcut tiles of the group were stored during the previous main chunk: one barrier
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
         u32x4 sf[16];
         auto sread = [&](int i) { sf[i] = *(const u32x4*)(smem + scb + sbuf * SCBYTES + i * 1024); };
 #pragma unroll
