@@ -195,6 +195,13 @@ int snrse_temb_dense(const float* temb, const float* W, const float* bias, float
 int snrse_input_conv(snrse_ctx* ctx, const void* x, const void* y, int B, int H, int W, const void* wgt, const float* bias,
                      void* out, float* pyr, double* stats, hipStream_t stream);
 
+/* The same input conv for the fp32x3 parity mode: wgt = ops.split_weight of the packed [128][64] weights ([128][128]
+ * bf16: per 32-element K tile 32 hi then 32 lo), split-bf16 products (w_hi.x_hi + w_lo.x_hi + w_hi.x_lo), f32 out
+ * [B*H*W][128]; the input rows staged in LDS (W % 64 == 0, W <= 1024, (H*W/64) % 16 == 0).  Replaces
+ * snrse_input_pack + the split GEMM on its im2col. */
+int snrse_input_conv_x3(snrse_ctx* ctx, const void* x, const void* y, int B, int H, int W, const void* wgt,
+                        const float* bias, float* out, float* pyr, double* stats, hipStream_t stream);
+
 /* Network input (ncsnpp.py:253-254, 282-285): complex x, y [B,F,T] -> im2col [B,F,T,64]
  * (tap-major 3x3 x {x.re, x.im, y.re, y.im}, zero padded) in dtype, and the f32 input
  * pyramid [B,F,T,4]. */

@@ -437,6 +437,129 @@ __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __res
   unsafeAtomicAdd(&stats[stat_idx(b, slot, tid >> 1, 128) + (tid & 1)], (double)tot);
 }
 
+// ---- the fp32x3 parity mode's input conv: the same LDS staging, split-bf16 products, fp32 output --------------
+// (replaces input_pack's fp32 im2col round trip through HBM + the split GEMM on it.)  Each tap value is split as the
+// split GEMMs split activations (hi = bf16(x), lo = bf16(x - hi)), the packed weights come pre-split per 32-element
+// K tile (ops.split_weight: 32 hi then 32 lo), and every 16x16x32 block accumulates w_hi.x_hi + w_lo.x_hi + w_hi.x_lo.
+// Channels split over wave pairs as input_conv_lds_kernel<64> (4 channel blocks per wave); a lane stores its 4
+// consecutive f32 channels of one pixel as one 16-B vector.  W <= 1024, as the bf16 form.
+__global__ __launch_bounds__(256) void input_conv_lds_x3_kernel(const float2* __restrict__ x,
+                                                                const float2* __restrict__ y, int H, int W,
+                                                                const bf16_t* __restrict__ wgt,
+                                                                const float* __restrict__ bias, float* __restrict__ out,
+                                                                float* __restrict__ pyr, double* __restrict__ stats) {
+  constexpr int NJ = 4, TPS = 8;
+  extern __shared__ __attribute__((aligned(16))) char ic_smem[];
+  __shared__ float s_st[2][128 * 2];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, lr = lane & 15;
+  const int ps = wid >> 1, jb = (wid & 1) * NJ;
+  const int HW = H * W, tpr = W / 64;
+  const long long p0 = (long long)blockIdx.x * 1024;
+  const int b = (int)(p0 / HW);
+  const size_t img = (size_t)b * HW;
+  const int q0 = (int)(p0 - (long long)b * HW);
+  const int r0 = q0 / W - 1, nrows = (q0 + 1023) / W + 2 - r0;
+  float4* st = (float4*)ic_smem;
+  const int npair = nrows * W / 2;
+  for (int i = tid; i < npair; i += 256) {
+    const int rr = (2 * i) / W, cc = 2 * i - rr * W, ih = r0 + rr;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
+    if ((unsigned)ih < (unsigned)H) {
+      a = *(const float4*)(x + img + (size_t)ih * W + cc);
+      c = *(const float4*)(y + img + (size_t)ih * W + cc);
+    }
+    st[2 * i] = make_float4(a.x, a.y, c.x, c.y);
+    st[2 * i + 1] = make_float4(a.z, a.w, c.z, c.w);
+  }
+  u32x4 wh[NJ][2], wl[NJ][2];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16_t* wr = wgt + (16 * (jb + j) + lr) * 128 + 64 * s + 8 * g;
+      wh[j][s] = *(const u32x4*)wr;
+      wl[j][s] = *(const u32x4*)(wr + 32);
+    }
+  f32x4 bv[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) bv[j] = *(const f32x4*)(bias + 16 * (jb + j) + 4 * g);
+  float s1[NJ][4], s2[NJ][4];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { s1[j][e] = 0.f; s2[j][e] = 0.f; }
+  int tdy[3], tdx[3];
+  bool tuse[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int tap = u < 2 ? 2 * g + u : 8;
+    tuse[u] = u < 2 || g == 0;
+    tdy[u] = tap / 3 - 1;
+    tdx[u] = tap % 3 - 1;
+  }
+  __syncthreads();
+  const int tile0 = q0 / 64 + ps * TPS;
+  for (int q = 0; q < 4 * TPS; ++q) {
+    const int tile = tile0 + (q >> 2);
+    const int h = tile / tpr, w = (tile - h * tpr) * 64 + 16 * (q & 3) + lr;
+    float4 v[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int hh = h + tdy[u], ww = w + tdx[u];
+      const bool ok = tuse[u] && (unsigned)ww < (unsigned)W;
+      const float4 t = st[(hh - r0) * W + (ok ? ww : w)];
+      v[u] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    u32x4 ph[2], pl[2];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int sl = u < 2 ? 0 : 1, hw_ = u < 2 ? 2 * u : 0;
+      const float e4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const uint32_t hi = pack_bf16x2(e4[2 * k], e4[2 * k + 1]);
+        ph[sl][hw_ + k] = hi;
+        pl[sl][hw_ + k] = pack_bf16x2(e4[2 * k] - __uint_as_float(hi << 16),
+                                      e4[2 * k + 1] - __uint_as_float(hi & 0xffff0000u));
+      }
+    }
+    ph[1][2] = ph[1][3] = pl[1][2] = pl[1][3] = 0u;
+    if (g == 2 && jb == 0) *(float4*)(pyr + (img + (size_t)h * W + w) * 4) = v[0];
+    float* orow = out + (img + (size_t)h * W + w) * 128 + 4 * g;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        acc = mfma_bf16_16x16x32(wh[j][s], ph[s], acc);
+        acc = mfma_bf16_16x16x32(wl[j][s], ph[s], acc);
+        acc = mfma_bf16_16x16x32(wh[j][s], pl[s], acc);
+      }
+      const f32x4 o = acc + bv[j];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s1[j][e] += o[e];
+        s2[j][e] = fmaf(o[e], o[e], s2[j][e]);
+      }
+      *(f32x4*)(orow + 16 * (jb + j)) = o;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a = ic_row_sum16(s1[j][e]), qq = ic_row_sum16(s2[j][e]);
+      if (lr == 0) {
+        s_st[ps][(16 * (jb + j) + 4 * g + e) * 2] = a;
+        s_st[ps][(16 * (jb + j) + 4 * g + e) * 2 + 1] = qq;
+      }
+    }
+  __syncthreads();
+  const int slot = blockIdx.x & (SNRSE_STAT_SLOTS - 1);
+  unsafeAtomicAdd(&stats[stat_idx(b, slot, tid >> 1, 128) + (tid & 1)], (double)(s_st[0][tid] + s_st[1][tid]));
+}
+
 // ---- Philox4x32-10 -> Box-Muller complex normals -------------------------------------
 SNRSE_DEV uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t& hi) {
   const uint64_t p = (uint64_t)a * b;
@@ -607,6 +730,23 @@ extern "C" int snrse_input_conv(snrse_ctx* ctx, const void* x, const void* y, in
   }
   hipLaunchKernelGGL(input_conv_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const float2*)x, (const float2*)y,
                      H, W, (const bf16_t*)wgt, bias, (bf16_t*)out, pyr, stats);
+  return (int)hipGetLastError();
+}
+
+extern "C" int snrse_input_conv_x3(snrse_ctx* ctx, const void* x, const void* y, int B, int H, int W, const void* wgt,
+                                   const float* bias, float* out, float* pyr, double* stats, hipStream_t s) {
+  if (B <= 0 || H <= 0 || W <= 0 || W % 64 || W > 1024 || ((long long)H * W / 64) % 16 || !x || !y || !wgt || !bias ||
+      !out || !pyr || !stats)
+    return SNRSE_EINVAL;
+  if (!snrse_ctx_resolve(ctx)->stats_zeroed)
+    SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * 128, s));
+  const long long blocks = (long long)B * H * W / (64 * 16);
+  const size_t lds = (size_t)(1023 / W + 4) * W * 16;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)input_conv_lds_x3_kernel,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+  SNRSE_RET(attr);
+  hipLaunchKernelGGL(input_conv_lds_x3_kernel, dim3((unsigned)blocks), dim3(256), lds, s, (const float2*)x,
+                     (const float2*)y, H, W, (const bf16_t*)wgt, bias, out, pyr, stats);
   return (int)hipGetLastError();
 }
 

@@ -285,6 +285,9 @@ class NCSNppHIP:
         if self.dtype == torch.bfloat16 and ops.input_conv_ok(x) and not _NO_FUSED_INPUT:
             ht, hst, pyr_in = ops.input_conv(x, y, W["in_w"], W["in_b"])
             h = (ht, hst)
+        elif self.gemm == "x3" and ops.input_conv_x3_ok(x) and not _NO_FUSED_INPUT:
+            ht, hst, pyr_in = ops.input_conv_x3(x, y, W["in_w"], W["in_b"])  # (W["in_w"]: split weights)
+            h = (ht, hst)
         else:
             col, pyr_in = ops.input_pack(x, y, self.dtype)
             h = self._conv(col, W["in_w"], 1, 128, bias=W["in_b"])

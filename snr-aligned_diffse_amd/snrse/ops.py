@@ -505,6 +505,25 @@ def input_conv(x, y, wgt, bias):
     return h, st, pyr
 
 
+def input_conv_x3_ok(x):
+    return input_conv_ok(x) and x.shape[-1] <= 1024
+
+
+def input_conv_x3(x, y, wgt_split, bias):
+    """fp32x3 fused input conv: x, y complex64 [B,F,T], split weights [128][128] bf16 -> (h [B,F,T,128] f32,
+    stats, pyramid f32)."""
+    _dev(x, y, wgt_split, bias)
+    B, F, T = x.shape[0], x.shape[-2], x.shape[-1]
+    h = torch.empty(B, F, T, 128, device=x.device, dtype=torch.float32)
+    pyr = torch.empty(B, F, T, 4, device=x.device, dtype=torch.float32)
+    st = new_stats(B, 128)
+    cx = context(x.device)
+    _stats_zeroed(cx, st)
+    _lib.call("snrse_input_conv_x3", cx.ptr, x.data_ptr(), y.data_ptr(), B, F, T, wgt_split.data_ptr(),
+              bias.data_ptr(), h.data_ptr(), pyr.data_ptr(), st.data_ptr(), _stream())
+    return h, st, pyr
+
+
 def input_pack(x, y, dtype):
     """x, y complex64 [B,F,T] -> (im2col [B,F,T,64] dtype, pyramid [B,F,T,4] f32)."""
     _dev(x, y)

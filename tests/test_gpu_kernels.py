@@ -691,6 +691,36 @@ def test_input_conv_fused_vs_im2col_gemm(gpu):
     assert not ops.input_conv_ok(ok_shape)  # 8 x 64 px = 8 tiles: outside the contract
 
 
+@pytest.mark.parametrize("shape", [(2, 256, 128), (1, 16, 64), (1, 256, 384), (1, 48, 320)])
+def test_input_conv_x3_vs_pack_and_split_gemm(gpu, shape):
+    """The fp32x3 fused input conv (snrse_input_conv_x3: LDS-staged rows, split-bf16 products, f32 out; the fp32
+    parity mode's ncsnpp.py:282-285) against the path it replaces -- input_pack's fp32 im2col + the split GEMM on the
+    same split weights -- to 1e-5 relative (only the accumulation order differs), the statistics to 1e-5, the
+    pyramid exactly; and against a float64 conv of the fp32 inputs and weights to 3e-5 (the split GEMMs' bound)."""
+    from snrse import ops
+    B, F, T = shape
+    g = torch.Generator().manual_seed(7 * F + T)
+    x = torch.complex(torch.randn(B, F, T, generator=g), torch.randn(B, F, T, generator=g)).to(gpu)
+    y = torch.complex(torch.randn(B, F, T, generator=g), torch.randn(B, F, T, generator=g)).to(gpu)
+    w = torch.randn(128, 36, generator=g) / 6
+    wp = torch.cat([w, torch.zeros(128, 28)], 1).to(gpu).contiguous()
+    ws = ops.split_weight(wp)
+    bias = (torch.randn(128, generator=g) * 0.1).to(gpu)
+    assert ops.input_conv_x3_ok(x)
+    h, st, pyr = ops.input_conv_x3(x, y, ws, bias)
+    col, pyr0 = ops.input_pack(x, y, torch.float32)
+    st0 = ops.new_stats(B, 128)
+    h0 = ops.conv2d(col, ws, 1, 128, bias=bias, stats=st0)
+    torch.cuda.synchronize()
+    assert h.dtype == torch.float32 and torch.equal(pyr, pyr0)
+    assert rel(h, h0) < 1e-5, rel(h, h0)
+    assert rel(st.sum(1), st0.sum(1)) < 1e-5
+    xin = torch.stack([x.real, x.imag, y.real, y.imag], 1).double().cpu()
+    wt = w.double().reshape(128, 3, 3, 4).permute(0, 3, 1, 2)
+    ref = torch.nn.functional.conv2d(xin, wt, bias.double().cpu(), padding=1).permute(0, 2, 3, 1)
+    assert rel(h.cpu(), ref) < 3e-5, rel(h.cpu(), ref)
+
+
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("shape", [(2, 256, 128), (1, 16, 64), (1, 256, 384), (1, 64, 1024), (2, 32, 512), (1, 48, 320)])
 def test_input_conv_lds_staged_matches_streaming(gpu, shape, mode):
