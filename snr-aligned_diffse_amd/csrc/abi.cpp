@@ -60,6 +60,7 @@ int* option_field(snrse_ctx& c, const char* name) {
   if (name_is(name, "h10")) return &c.h10;
   if (name_is(name, "ic_lds")) return &c.ic_lds;
   if (name_is(name, "x3_nt")) return &c.x3_nt;
+  if (name_is(name, "x3_tw")) return &c.x3_tw;
   return nullptr;
 }
 

@@ -101,6 +101,7 @@ struct snrse_ctx {
   int resample_nt = 0;         // non-temporal stores in gn_resample
   int resample_down_rows = 4;  // output rows per down-sampling row strip (1, 2, 4; 4 fastest since r03)
   int x3_tile = 0;             // split-bf16 fp32 GEMM tile: 0 auto, 1 128x128, 2 256x128, 3 128x256, 4 halo
+  int x3_tw = 0;               // fp32x3 halo GEMM tile: 0 auto (8 x 32 where H % 8 == 0, W % 32 == 0), 64 = 4 x 64
   int x3_nt = 0;               // fp32x3 halo GEMM: non-temporal output stores by the epi_nt rule (A/B)
   int x3_spread = 1;           // halo split GEMM: next chunk's halo stored one piece per tap (0: in one go)
   int ic_lds = 1;              // bf16 input conv: 1 the workgroup's input rows staged in LDS (W <= 1024), 2 the same

@@ -777,14 +777,24 @@ constexpr size_t LDS_MAIN = 2 * (size_t)HBYTES + 3 * (size_t)TAPB;
 constexpr size_t LDS_EPI = 8 * (64 * 68 * 4) + 4 * 128 * 2 * 4;
 constexpr size_t LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
 }  // namespace x3h
+// the same geometry for tile width TW (64: 4 x 64 px, the namespace above; 32: 8 x 32 px, 340 halo rows per 256
+// pixels instead of 396 -- 14 % less halo to load, split and GroupNorm per output, as v5's 8 x 32 form)
+template <int TW_>
+struct X3G {
+  static constexpr int TW = TW_, TH = 256 / TW_, HC = TW_ + 2, HROWS = (TH + 2) * HC;
+  static constexpr int HBYTES = HROWS * 128, HJ = (HROWS * 8 + 511) / 512, TAPB = x3h::TAPB;
+  static constexpr int RW = 64 / TW_;  // image rows of a wave's 64 pixels
+  static constexpr size_t LDS_MAIN = 2 * (size_t)HBYTES + 3 * (size_t)TAPB;
+  static constexpr size_t LDS = LDS_MAIN > x3h::LDS_EPI ? LDS_MAIN : x3h::LDS_EPI;
+};
 
 // s_waitcnt vmcnt(n) for the counts the x3h schedule produces (anything else waits for all)
 SNRSE_DEV void x3h_vm_wait(int n) {
   switch (n) {
 #define SNRSE_X3H_VM(N) \
   case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-    SNRSE_X3H_VM(2) SNRSE_X3H_VM(7) SNRSE_X3H_VM(9) SNRSE_X3H_VM(11) SNRSE_X3H_VM(14) SNRSE_X3H_VM(16)
-    SNRSE_X3H_VM(18) SNRSE_X3H_VM(20)
+    SNRSE_X3H_VM(2) SNRSE_X3H_VM(6) SNRSE_X3H_VM(7) SNRSE_X3H_VM(8) SNRSE_X3H_VM(9) SNRSE_X3H_VM(10)
+    SNRSE_X3H_VM(11) SNRSE_X3H_VM(12) SNRSE_X3H_VM(14) SNRSE_X3H_VM(16) SNRSE_X3H_VM(18) SNRSE_X3H_VM(20)
 #undef SNRSE_X3H_VM
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
@@ -792,9 +802,11 @@ SNRSE_DEV void x3h_vm_wait(int n) {
 
 // GNM: GroupNorm prologue of the main input as in the bf16 halo kernel (0 none, 1 affine, 2 affine +
 // SiLU), applied once per halo element while it is split: the fp32 mode's gn_act pass disappears.
-template <int GNM, bool SPR>
+template <int GNM, bool SPR, int TWV>
 __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
-  using namespace x3h;
+  using G = X3G<TWV>;
+  constexpr int TH = G::TH, TW = G::TW, HC = G::HC, HROWS = G::HROWS, HBYTES = G::HBYTES, HJ = G::HJ;
+  constexpr int TAPB = G::TAPB, RW = G::RW;
   constexpr int HOPS = HJ + (GNM > 0 ? 2 : 0);  // vector-memory ops of one halo prefetch per thread
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const ring = smem + 2 * HBYTES;
@@ -959,12 +971,14 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
   // one tap's fragment reads + 48 MFMAs from halo buffer hb and ring slot sb
   auto tap_mfma = [&](const char* hb, const char* sb, int tp) {
     const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
-    const int hbase = (wr + dy + 1) * HC + dx + 1 + lrow;
+    // fragment i: the wave's pixels 16 i .. 16 i + 15 = image row wr RW + 16 i / TW, columns (16 i) % TW ..
+    const int hbase = (wr * RW + dy + 1) * HC + dx + 1 + lrow;
     u32x4 ah[4], al[4], bh[4], bl[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      ah[i] = *(const u32x4*)(hb + swz(hbase + 16 * i, lg));
-      al[i] = *(const u32x4*)(hb + swz(hbase + 16 * i, 4 + lg));
+      const int hr = hbase + (16 * i / TW) * HC + (16 * i) % TW;
+      ah[i] = *(const u32x4*)(hb + swz(hr, lg));
+      al[i] = *(const u32x4*)(hb + swz(hr, 4 + lg));
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1002,7 +1016,7 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
         wload(q + 2);
         if (tp == 0) halo_load(c + 1 < ncb ? c + 1 : c);
         tap_mfma(hb, ring + (q % 3) * TAPB, tp);
-        if (tp >= 2) halo_piece(nb_, tp - 2, tr);
+        if (tp >= 2 && tp - 2 < HJ) halo_piece(nb_, tp - 2, tr);
       }
     }
     for (int c = cbm; c < ncb; ++c, ++q) {
@@ -1032,12 +1046,14 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
     const char* hb = smem + (c & 1) * HBYTES;
     const char* sb = ring + (q % 3) * TAPB;
     const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
-    const int hbase = (wr + dy + 1) * HC + dx + 1 + lrow;
+    // fragment i: the wave's pixels 16 i .. 16 i + 15 = image row wr RW + 16 i / TW, columns (16 i) % TW ..
+    const int hbase = (wr * RW + dy + 1) * HC + dx + 1 + lrow;
     u32x4 ah[4], al[4], bh[4], bl[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      ah[i] = *(const u32x4*)(hb + swz(hbase + 16 * i, lg));
-      al[i] = *(const u32x4*)(hb + swz(hbase + 16 * i, 4 + lg));
+      const int hr = hbase + (16 * i / TW) * HC + (16 * i) % TW;
+      ah[i] = *(const u32x4*)(hb + swz(hr, lg));
+      al[i] = *(const u32x4*)(hb + swz(hr, 4 + lg));
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1065,9 +1081,13 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // LDS is reused as the epilogue staging area
-  const int mb = (bb * p.H + h0 + wr) * p.W + w0;
-  epilogue_lds<float, 4, 128>(p, acc, mb, n0 + wc * 64, lane, (float*)(smem + wid * (64 * 68 * 4)),
-                              (float*)(smem + 8 * (64 * 68 * 4)), wr, bb, n0, min(TW, p.W - w0));
+  const int mb = (bb * p.H + h0 + wr * RW) * p.W + w0;
+  if constexpr (TW == 64)
+    epilogue_lds<float, 4, 128>(p, acc, mb, n0 + wc * 64, lane, (float*)(smem + wid * (64 * 68 * 4)),
+                                (float*)(smem + 8 * (64 * 68 * 4)), wr, bb, n0, min(TW, p.W - w0));
+  else  // two 32-px row segments per wave (W % 32 == 0: no cut tiles)
+    epilogue_img<float, 4, 128, false, EF_RT, TW>(p, acc, mb, n0 + wc * 64, lane, (float*)(smem + wid * (64 * 68 * 4)),
+                                                 (float*)(smem + 8 * (64 * 68 * 4)), wr, bb, n0, p.W - TW);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1725,26 +1745,28 @@ int launch_x3(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   return (int)hipGetLastError();
 }
 
-template <int GNM, bool SPR>
+template <int GNM, bool SPR, int TWV>
 int launch_x3h_gn(ConvParams p, hipStream_t s, int tiles) {
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_x3h_kernel<GNM, SPR>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)x3h::LDS);
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_x3h_kernel<GNM, SPR, TWV>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)X3G<TWV>::LDS);
   SNRSE_RET(attr);
   p.ntn = p.Cout / 128;
   p.ksplit = 1;
-  hipLaunchKernelGGL((conv_x3h_kernel<GNM, SPR>), dim3(tiles), dim3(512), x3h::LDS, s, p);
+  hipLaunchKernelGGL((conv_x3h_kernel<GNM, SPR, TWV>), dim3(tiles), dim3(512), X3G<TWV>::LDS, s, p);
   return (int)hipGetLastError();
 }
 
-template <bool SPR>
+template <bool SPR, int TWV>
 int launch_x3h_spr(const ConvParams& p, hipStream_t s, int tiles) {
-  if (!p.gn_scale) return launch_x3h_gn<0, SPR>(p, s, tiles);
-  if (!p.gn_act) return launch_x3h_gn<1, SPR>(p, s, tiles);
-  return launch_x3h_gn<2, SPR>(p, s, tiles);
+  if (!p.gn_scale) return launch_x3h_gn<0, SPR, TWV>(p, s, tiles);
+  if (!p.gn_act) return launch_x3h_gn<1, SPR, TWV>(p, s, tiles);
+  return launch_x3h_gn<2, SPR, TWV>(p, s, tiles);
 }
 
-int launch_x3h(const ConvParams& p, hipStream_t s, int tiles, int spread) {
-  return spread ? launch_x3h_spr<true>(p, s, tiles) : launch_x3h_spr<false>(p, s, tiles);
+// tw 32: the 8 x 32 px tiles (H % 8 == 0, W % 32 == 0; tiles counted for them), else 4 x 64
+int launch_x3h(const ConvParams& p, hipStream_t s, int tiles, int spread, int tw) {
+  if (tw == 32) return spread ? launch_x3h_spr<true, 32>(p, s, tiles) : launch_x3h_spr<false, 32>(p, s, tiles);
+  return spread ? launch_x3h_spr<true, 64>(p, s, tiles) : launch_x3h_spr<false, 64>(p, s, tiles);
 }
 
 template <int BM, int BN, typename TO>
@@ -1913,7 +1935,11 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
         r.epi_nt = cx.x3_nt && (cx.epi_nt == 2 ? ((long long)q.M * q.out_ld * 4ll > ((long long)cx.epi_nt_mb << 20))
                                                : cx.epi_nt != 0);
         cx.last_epi_nt = r.epi_nt;
-        return launch_x3h(r, stream, x3h_tiles, cx.x3_spread);
+        // 8 x 32 tiles where they fit (option x3_tw: 0 auto, 64 forces 4 x 64)
+        const bool tw32 = cx.x3_tw != 64 && q.H % 8 == 0 && q.W % 32 == 0;
+        cx.last_tw = tw32 ? 32 : 64;
+        return launch_x3h(r, stream, tw32 ? q.B * (q.H / 8) * (q.W / 32) * (q.Cout / 128) : x3h_tiles, cx.x3_spread,
+                          tw32 ? 32 : 64);
       }
       if (q.Cout <= 16 && cx.conv_variant != 1 && head_ok(q)) {  // the pyramid heads, GroupNorm fused
         cx.last_kernel = 11;
