@@ -105,7 +105,8 @@ struct snrse_ctx {
   int x3_nt = 1;               // fp32x3 halo GEMM: non-temporal output stores by the epi_nt rule (+0.3 %, r04r)
   int x3_spread = 1;           // halo split GEMM: next chunk's halo stored one piece per tap (0: in one go)
   int ic_lds = 1;              // bf16 input conv: 1 the workgroup's input rows staged in LDS (W <= 1024), 2 the same
-                               // with the channels split over wave pairs (4 waves / SIMD), 0 streaming loads
+                               // with the channels split over wave pairs (4 waves / SIMD), 3 the output staged
+                               // through LDS for 1-KB contiguous stores, 0 streaming loads
   int h10 = 2;                 // v10 halo GEMM under conv_variant 0: 1 = every bf16 3x3 conv v5 takes (and v10x3 in
                                // fp32x3), 2 = the concatenated-input ones without a shortcut, 0 = off
   int num_cu = 0;              // compute units of the device (v10 persistent grid), read on first use

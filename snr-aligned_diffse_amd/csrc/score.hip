@@ -309,7 +309,10 @@ __global__ __launch_bounds__(256) void input_conv_kernel(const float2* __restric
 // ICH: output channels per wave (128: a wave owns 4 of the workgroup's 16 tiles; 64: waves (2 s, 2 s + 1) share pixel
 // stream s = 8 tiles and split the channels -- half the weight / bias / statistics registers, so more waves per SIMD
 // hide the store and LDS latency)
-template <int ICH>
+// SST (ICH 128): the block's 16 px x 128 ch output (4 KB, contiguous in NHWC) goes through a per-wave LDS stage
+// (16-B chunk c of pixel p at p * 256 + (c ^ (p & 15)) * 16: conflict-free 8-B writes and 16-B reads) and out as 4
+// fully contiguous 1-KB wave stores, instead of 4 stores of 64-B pieces of 16 pixels each
+template <int ICH, bool SST = false>
 __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __restrict__ x, const float2* __restrict__ y,
                                                              int H, int W, const bf16_t* __restrict__ wgt,
                                                              const float* __restrict__ bias, bf16_t* __restrict__ out,
@@ -340,6 +343,8 @@ __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __res
     st[2 * i] = make_float4(a.x, a.y, c.x, c.y);
     st[2 * i + 1] = make_float4(a.z, a.w, c.z, c.w);
   }
+  // output stage of this wave (SST): after the input rows of the largest launch ((1023 / W + 4) W 16 B)
+  char* const ostg = ic_smem + (size_t)(1023 / W + 4) * W * 16 + wid * 4096;
   u32x4 wf[NJ][2];
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
@@ -391,6 +396,7 @@ __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __res
     if (g == 2 && jb == 0)  // tap 4 = the pixel itself: the input pyramid (written by one wave of the stream)
       *(float4*)(pyr + (img + (size_t)h * W + w) * 4) = v[0];
     bf16_t* orow = out + (img + (size_t)h * W + w) * 128 + 8 * (g >> 1);
+    typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 #pragma unroll
     for (int jp = 0; jp < NJ / 2; ++jp) {
       uint32_t pk[2][2];
@@ -409,11 +415,25 @@ __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __res
         }
         pk[hh][0] = pack_bf16x2(vv[0], vv[1]);
         pk[hh][1] = pack_bf16x2(vv[2], vv[3]);
+        if constexpr (SST)  // channels 16 j + 4 g .. + 3 of pixel lr: half (g & 1) of 16-B chunk 2 j + (g >> 1)
+          *(u32x2*)(ostg + lr * 256 + (((2 * j + (g >> 1)) ^ lr) << 4) + (g & 1) * 8) = u32x2{pk[hh][0], pk[hh][1]};
       }
+      if constexpr (SST) continue;
       const auto a0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
       const auto a1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
       const u32x4 o = {a0[0], a1[0], a0[1], a1[1]};
       *(u32x4*)(orow + 16 * (jb + 2 * jp + (g & 1))) = o;
+    }
+    if constexpr (SST) {  // the block's 4 KB: pixel 4 k + (lane >> 4), 16-B chunk lane & 15, contiguous per wave store
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      bf16_t* ob = out + (img + (size_t)h * W + (w - lr)) * 128;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int pp = 4 * k + (lane >> 4), c = lane & 15;
+        const u32x4 o = *(const u32x4*)(ostg + pp * 256 + ((c ^ pp) << 4));
+        *(u32x4*)(ob + pp * 128 + c * 8) = o;
+      }
+      asm volatile("" ::: "memory");  // (the next block's stage writes follow these reads in the wave's LDS order)
     }
   }
   // statistics: s_st[pixel stream][channel][2] (each channel written by one wave per stream), then a fixed-order
@@ -720,7 +740,13 @@ extern "C" int snrse_input_conv(snrse_ctx* ctx, const void* x, const void* y, in
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
     SNRSE_RET(attr1);
     SNRSE_RET(attr2);
-    if (snrse_ctx_resolve(ctx)->ic_lds == 2)
+    static const hipError_t attr3 = hipFuncSetAttribute((const void*)input_conv_lds_kernel<128, true>,
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    SNRSE_RET(attr3);
+    if (snrse_ctx_resolve(ctx)->ic_lds == 3)
+      hipLaunchKernelGGL((input_conv_lds_kernel<128, true>), dim3((unsigned)blocks), dim3(256), lds + 4 * 4096, s,
+                         (const float2*)x, (const float2*)y, H, W, (const bf16_t*)wgt, bias, (bf16_t*)out, pyr, stats);
+    else if (snrse_ctx_resolve(ctx)->ic_lds == 2)
       hipLaunchKernelGGL(input_conv_lds_kernel<64>, dim3((unsigned)blocks), dim3(256), lds, s, (const float2*)x,
                          (const float2*)y, H, W, (const bf16_t*)wgt, bias, (bf16_t*)out, pyr, stats);
     else

@@ -721,10 +721,11 @@ def test_input_conv_x3_vs_pack_and_split_gemm(gpu, shape):
     assert rel(h.cpu(), ref) < 3e-5, rel(h.cpu(), ref)
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 @pytest.mark.parametrize("shape", [(2, 256, 128), (1, 16, 64), (1, 256, 384), (1, 64, 1024), (2, 32, 512), (1, 48, 320)])
 def test_input_conv_lds_staged_matches_streaming(gpu, shape, mode):
-    """The LDS-staged input conv (option ic_lds 1, or 2 with the channels split over wave pairs; W <= 1024: the
+    """The LDS-staged input conv (option ic_lds 1, 2 with the channels split over wave pairs, 3 with the output
+    staged too for whole-KB stores; W <= 1024: the
     workgroup's rows + 2 halo rows loaded once) writes the same h and pyramid bytes as the streaming form and the same
     statistics (mode 2 folds its f32 partial sums over other pixel groups: to 1e-5), including widths that do not
     divide the workgroup's 1024 pixels (W = 384, 320: a workgroup spans partial rows) and the first / last rows."""
@@ -745,7 +746,7 @@ def test_input_conv_lds_staged_matches_streaming(gpu, shape, mode):
             ops.set_option("ic_lds", 1)
     (h1, s1, p1), (h0, s0, p0) = outs
     assert torch.equal(h1, h0) and torch.equal(p1, p0)
-    tol = 1e-9 if mode == 1 else 1e-5
+    tol = 1e-5 if mode == 2 else 1e-9
     assert torch.allclose(s1.sum(1), s0.sum(1), rtol=tol, atol=tol * float(s0.sum(1).abs().max()))
 
 

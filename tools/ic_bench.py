@@ -31,7 +31,7 @@ def main():
     bias = torch.randn(128, device=dev, generator=g) * 0.1
     nbytes = B * F * T * (16 + 256 + 16)
     for r in range(a.rounds):
-        for v in (0, 1, 2):
+        for v in (0, 1, 2, 3):
             ops.set_option("ic_lds", v)
             ops.input_conv(x, y, wp, bias)
             s = torch.cuda.current_stream()
