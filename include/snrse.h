@@ -164,8 +164,9 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  * "h10" the v10 halo GEMM under conv_variant 0 (conv_variant 10 forces it): 2 (default) the concatenated-input
  *   3x3 convs without a shortcut, 1 every conv the v5 halo GEMM would take (and its split-bf16 form in the
  *   fp32x3 mode), 0 off;
- * "ic_lds" 1 (default) the bf16 input conv stages its workgroup's input rows in LDS (W <= 1024), 2 the same with
- *   the channels split over wave pairs, 0 the streaming form (bit-identical);
+ * "ic_lds" the bf16 input conv (W <= 1024): 3 (default) its workgroup's input rows staged in LDS and its output
+ *   staged through LDS for whole-KB stores, 1 input rows only, 2 with the channels split over wave pairs, 0 the
+ *   streaming form (all bit-identical but 2's statistics fold order);
  * "x3_tw" fp32x3 halo GEMM tile: 0 (default) 8 x 32 px where H % 8 == 0 and W % 32 == 0, else 4 x 64; 64 forces
  *   4 x 64; "x3_nt" 1 (default) its fp32 output stores non-temporal under the "epi_nt" rule. */
 int snrse_set_option(const char* name, int value);

@@ -743,7 +743,7 @@ def test_input_conv_lds_staged_matches_streaming(gpu, shape, mode):
         try:
             outs.append(ops.input_conv(x, y, wp, bias))
         finally:
-            ops.set_option("ic_lds", 1)
+            ops.set_option("ic_lds", 3)
     (h1, s1, p1), (h0, s0, p0) = outs
     assert torch.equal(h1, h0) and torch.equal(p1, p0)
     tol = 1e-5 if mode == 2 else 1e-9
