@@ -22,6 +22,8 @@ SHAPES = [
     (32, 256, 0, 256, 64, 128, 3, 0),
     (32, 256, 256, 256, 32, 64, 3, 0),
     (32, 256, 0, 768, 16, 32, 1, 0),
+    (32, 128, 0, 128, 256, 512, 3, 256),   # 7: up-path Conv_1 at level 0: shortcut over cat(h, skip) = 256 channels
+    (32, 256, 0, 256, 128, 256, 3, 512),   # 8: the same at level 1
 ]
 
 
