@@ -1,0 +1,48 @@
+"""CPU tests of the host-side agreement logic bench.py writes into its line (paritycheck.waveform_agreement:
+parity_mode.c2_agreement, bounded by paritycheck.C2_AGREE): per-clip SI-SDR as the reference computes it
+(sgmse/util/other.py:71-75) and the distribution bounds (median, fraction >= 25 dB, floor, mean relative RMS)."""
+import math
+
+import numpy as np
+import torch
+
+import paritycheck
+
+
+def _pair(n, snr_db, seed=0, L=4000):
+    g = torch.Generator().manual_seed(seed)
+    ref = torch.randn(n, L, generator=g, dtype=torch.float64)
+    noise = torch.randn(n, L, generator=g, dtype=torch.float64)
+    scale = torch.as_tensor(10 ** (-np.asarray(snr_db, dtype=np.float64) / 20))[:, None]
+    noise *= (ref.norm(dim=1, keepdim=True) / noise.norm(dim=1, keepdim=True)) * scale
+    return ref + noise, ref
+
+
+def test_si_sdr_matches_the_reference_formula():
+    est, ref = _pair(3, [10.0, 20.0, 30.0])
+    r = paritycheck.waveform_agreement(est, ref, per_clip=True)
+    for k in range(3):
+        e, x = est[k], ref[k]
+        alpha = float((e * x).sum() / (x * x).sum())
+        want = 10 * math.log10(float((alpha * x).pow(2).sum() / (alpha * x - e).pow(2).sum()))
+        assert abs(r["per_clip"]["si_sdr_db"][k] - want) < 0.01
+    assert abs(r["si_sdr_bf16_vs_x3_db_median"] - 20.0) < 0.5
+
+
+def test_bounds_accept_one_outlier_and_reject_a_shifted_distribution():
+    snr = np.full(32, 32.0)
+    snr[0] = 11.0  # the measured outlier (profiles/r04d_agree_diag.json)
+    est, ref = _pair(32, snr)
+    ok = paritycheck.waveform_agreement(est, ref)
+    assert ok["ok"] and ok["frac_clips_ge_25db"] > 0.95 and ok["si_sdr_bf16_vs_x3_db_min"] < 12
+    # every clip 24 dB: median and fraction bounds fail
+    est, ref = _pair(32, np.full(32, 24.0))
+    assert not paritycheck.waveform_agreement(est, ref)["ok"]
+    # one clip diverged outright (below the 5 dB floor)
+    snr[3] = 2.0
+    est, ref = _pair(32, snr)
+    assert not paritycheck.waveform_agreement(est, ref)["ok"]
+    # NaN output anywhere
+    est, ref = _pair(32, np.full(32, 32.0))
+    est[5, 7] = float("nan")
+    assert not paritycheck.waveform_agreement(est, ref)["ok"]
