@@ -162,8 +162,8 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  * "stats_zeroed" 1 = the statistics buffers handed to snrse_conv2d / snrse_gn_stats are already zero (the
  * caller clears one arena per network evaluation), so they skip their per-call memset;
  * "h10" the v10 halo GEMM under conv_variant 0 (conv_variant 10 forces it): 2 (default) the concatenated-input
- *   3x3 convs without a shortcut, 1 every conv the v5 halo GEMM would take (and its split-bf16 form in the
- *   fp32x3 mode), 0 off;
+ *   3x3 convs without a shortcut, 3 those and the convs whose fused 1x1 shortcut spans twice their input
+ *   channels, 1 every conv the v5 halo GEMM would take (and its split-bf16 form in the fp32x3 mode), 0 off;
  * "ic_lds" the bf16 input conv (W <= 1024): 3 (default) its workgroup's input rows staged in LDS and its output
  *   staged through LDS for whole-KB stores, 1 input rows only, 2 with the channels split over wave pairs, 0 the
  *   streaming form (all bit-identical but 2's statistics fold order);

@@ -1811,7 +1811,11 @@ int dispatch_conv(const ConvParams& p, hipStream_t s, snrse_ctx& cx) {
           // v10 (conv_h10.hip): forced by conv_variant 10; taken by variant 0 on v5's shapes under option h10 = 1, and under
           // h10 = 2 for the concatenated-input convs without a shortcut (the up path's Conv_0, where it measured ~4 %
           // faster than v5: 8 chunks per tile amortise its epilogue; profiles/r04_v10_ablations.jsonl)
-          const bool h10_auto = cx.conv_variant == 0 && halo_tile64(p) && (cx.h10 == 1 || (cx.h10 == 2 && p.C1 > 0 && !p.sc_src));
+          // h10 = 3 adds the convs whose fused shortcut spans twice their input (the up path's Conv_1 over cat(h, skip))
+          const bool h10_cat = p.C1 > 0 && !p.sc_src;
+          const bool h10_sc2 = p.sc_src && p.Csc + p.Csc1 == 2 * (p.C0 + p.C1);
+          const bool h10_auto = cx.conv_variant == 0 && halo_tile64(p) &&
+                                (cx.h10 == 1 || (cx.h10 == 2 && h10_cat) || (cx.h10 == 3 && (h10_cat || h10_sc2)));
           if ((cx.conv_variant == 10 || h10_auto) && h10_ok(p)) {
             if (!cx.num_cu) {
               int dev = 0;

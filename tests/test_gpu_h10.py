@@ -142,3 +142,21 @@ def test_h10_nontemporal_epilogue_matches(gpu, case):
     assert torch.equal(outs[0][0], outs[1][0])
     if outs[0][1] is not None:
         assert rel(ops.fold_stats(outs[0][1]), ops.fold_stats(outs[1][1])) < 1e-12
+
+
+@pytest.mark.parametrize("h10,case,want", [(3, CASES[8], "conv_halo10_kernel"), (3, CASES[9], "conv_halo5_kernel"),
+                                           (2, CASES[8], "conv_halo5_kernel"), (3, CASES[2], "conv_halo10_kernel")])
+def test_h10_auto_dispatch(gpu, h10, case, want):
+    """Option h10 under conv_variant 0: 2 takes v10 for the concatenated-input convs without a shortcut, 3 also
+    for the convs whose shortcut spans twice their input (the up path's Conv_1 over cat(h, skip)); the result is
+    the same conv either way."""
+    from snrse import ops
+    ref, run = _case(gpu, case)
+    old = ops.get_option("h10")
+    ops.set_option("h10", h10)
+    try:
+        out, _, ran = run(0)
+    finally:
+        ops.set_option("h10", old)
+    assert ran == want
+    assert rel(out.float().permute(0, 3, 1, 2), ref) < 1e-2
