@@ -780,3 +780,30 @@ def test_gn_resample_down_rows(gpu, shape):
         assert rel(nchw(a.float()), ref_a) < 1e-2, rd
         assert rel(nchw(r.float()), ref_r) < 1e-2, rd
         assert torch.equal(a, outs[1][0]) and torch.equal(r, outs[1][1]), rd
+
+
+@pytest.mark.parametrize("C0,C1,groups", [(128, 0, None), (256, 0, None), (256, 128, None), (512, 0, None),
+                                          (64, 64, 16), (128, 256, 32), (1024, 0, None), (1024, 512, None)])
+def test_gn_scale_shift_matches_fp64(gpu, C0, C1, groups):
+    """snrse_gn_scale_shift against the GroupNorm affine computed in fp64 from the same bf16 activations
+    (reference GroupNorm: torch.nn.GroupNorm in ResnetBlockBigGANpp, layerspp.py:244-276; eps 1e-6), with split
+    (concatenated) inputs and group sizes that are not powers of two."""
+    from snrse import ops
+    B, H, W = 5, 16, 24
+    g = torch.Generator(device=gpu).manual_seed(C0 + 3 * C1)
+    x0 = (torch.randn(B, H, W, C0, device=gpu, generator=g) * 0.7 + 0.3).bfloat16()
+    x1 = (torch.randn(B, H, W, C1, device=gpu, generator=g) * 1.4 - 0.2).bfloat16() if C1 else None
+    gam = torch.rand(C0 + C1, device=gpu, generator=g) + 0.5
+    bet = torch.randn(C0 + C1, device=gpu, generator=g)
+    sums = ops.gn_stats(x0, x1)
+    C = C0 + C1
+    G = groups if groups is not None else min(C // 4, 32)
+    xs = x0.double() if x1 is None else torch.cat([x0, x1], -1).double()
+    xg = xs.reshape(B, H * W, G, C // G)
+    mean = xg.mean((1, 3))
+    rstd = (xg.var((1, 3), unbiased=False) + 1e-6).rsqrt()
+    scl_ref = rstd.repeat_interleave(C // G, 1) * gam.double()
+    sh_ref = bet.double() - mean.repeat_interleave(C // G, 1) * scl_ref
+    scl, sh = ops.gn_scale_shift(sums[0], gam, bet, H * W, sums1=sums[1], groups=groups)
+    assert torch.allclose(scl.double(), scl_ref, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(sh.double(), sh_ref, rtol=1e-5, atol=1e-5)
