@@ -1823,6 +1823,8 @@ int dispatch_conv(const ConvParams& p, hipStream_t s, snrse_ctx& cx) {
               SNRSE_RET(hipDeviceGetAttribute(&cx.num_cu, hipDeviceAttributeMultiprocessorCount, dev));
             }
             cx.last_kernel = 12;
+            cx.last_tw = kH10TileW;
+            cx.last_ksplit = 1;
             ConvParams q = p;  // (non-temporal output stores as the v5 launch decides them)
             q.epi_nt = cx.epi_nt == 2 ? ((long long)p.M * p.out_ld * 2ll > ((long long)cx.epi_nt_mb << 20)) : cx.epi_nt;
             cx.last_epi_nt = q.epi_nt;
@@ -1919,17 +1921,6 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
   auto run = [&](const ConvParams& q) {
     if (x3) {
       const int x3h_tiles = q.B * (q.H / x3h::TH) * ((q.W + x3h::TW - 1) / x3h::TW) * (q.Cout / 128);
-      // the v10 structure's split-bf16 form (option h10) on the x3h kernel's shapes where its 8 x 32 tiles fit
-      if (cx.h10 == 1 && x3h_all && h10x3_ok(q)) {
-        if (!cx.num_cu) {
-          int dev = 0;
-          SNRSE_RET(hipGetDevice(&dev));
-          SNRSE_RET(hipDeviceGetAttribute(&cx.num_cu, hipDeviceAttributeMultiprocessorCount, dev));
-        }
-        cx.last_kernel = 13;
-        cx.last_ksplit = 1;
-        return launch_h10x3(q, stream, cx.num_cu);
-      }
       if (x3h_all) {
         cx.last_kernel = 4;
         cx.last_ksplit = 1;

@@ -94,10 +94,8 @@ SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
 int launch_head(const ConvParams& p, hipStream_t s);
 // v10 halo GEMM (conv_h10.hip): persistent, one wave per SIMD, 16 x 32 px x 128 cout tiles, fused 1x1 shortcut
 bool h10_ok(const ConvParams& p);
+constexpr int kH10TileW = 32;  // its tile width (snrse_get_option "last_tw")
 int launch_h10(ConvParams p, hipStream_t s, int num_cu, bool specialise);
-// its split-bf16 form for the fp32x3 parity mode (conv_h10x3.hip): 8 x 32 px x 128 cout tiles
-bool h10x3_ok(const ConvParams& p);
-int launch_h10x3(ConvParams p, hipStream_t s, int num_cu);
 int launch_head_x3(const ConvParams& p, hipStream_t s);
 bool head_ok(const ConvParams& p);
 

@@ -28,7 +28,7 @@ using namespace snrse_conv;
 
 namespace {
 namespace h10 {
-constexpr int TH = 16, TW = 32, HC = TW + 2;
+constexpr int TH = 16, TW = kH10TileW, HC = TW + 2;
 constexpr int HROWS = (TH + 2) * HC;     // 612
 constexpr int HBYTES = HROWS * 64;       // 39168
 constexpr int VPT = (HROWS * 4 + 255) / 256;  // 10 halo vectors (16 B) per thread: vector tid + 256 k
@@ -44,15 +44,6 @@ constexpr int STRIDE = 10, XF0 = 40, LOAD0 = XF0 - 32;
 static_assert(XF0 + STRIDE * (VPT - 1) + 9 <= 144, "transform schedule fits one chunk");
 // up to two shortcut chunks' tiles (2 x 8 vectors per thread) loaded every SCSTRIDE steps from SCL0, stored SCLAG later
 constexpr int SCSTRIDE = 6, SCL0 = 4, SCLAG = 30;
-// weight prefetch distance in taps (2: the tap-start wait on a weight fragment no longer covers the halo loads of the
-// previous tap, vmcnt being in-order) and the halo loads' placement (early: all ten in steps 1-4, right after tap 0's
-// weight load, so ~40 steps before the first wait that covers them) -- shortcut-free instances only
-#ifndef H10_WD
-#define H10_WD 1
-#endif
-#ifndef H10_EARLY
-#define H10_EARLY 0
-#endif
 static_assert(SCL0 + SCSTRIDE * 15 + SCLAG < 144, "shortcut schedule fits one chunk");
 
 // single VALU instructions as asm statements: with the MFMAs also in asm (program order of volatile asm is kept),
@@ -101,14 +92,6 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
   const int g = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
   const int t_begin = (int)((long long)g * ntiles / nb), t_end = (int)((long long)(g + 1) * ntiles / nb);
   if (t_begin >= t_end) return;
-#ifdef H10_STAGGER  // experiment: workgroups start in 4 phases H10_STAGGER x 10 ns apart, so their epilogues (which write
-                    // 128 KB each) do not all fall in the same interval
-  {
-    const long long t0 = __builtin_amdgcn_s_memrealtime();
-    const long long dt = (long long)(bid & 3) * H10_STAGGER;
-    while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
-  }
-#endif
 
   const int H = p.H, W = p.W;
   const int ntw = W / TW, nth = H / TH;
@@ -146,20 +129,22 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
   // ---- per-thread halo vectors of a tile: row (tid >> 2) + 64 k, 16-B chunk tid & 3 (8 channels)
   const int hcol = tid & 3;
   // pixel index of each vector; outside the image (the conv's zero padding) or past the halo: -1.  Branch-free
-  // (unsigned range tests, no short-circuit): per-vector exec masks would pin 20 SGPRs across the main loop
-  int hyx[VPT];  // halo row / column of vector k: hy * 64 + hx (hy = 63: past the halo)
+  // (unsigned range tests, no short-circuit): per-vector exec masks would pin 20 SGPRs across the main loop.  A
+  // vector past the halo (only k = VPT - 1 can be) gets a column beyond any image (hx = 1 << 20), so it takes the
+  // out-of-range path (its buffer load reads zeros without touching memory, its store is skipped)
+  int hyx[VPT];  // halo row / column of vector k: hy * 64 + hx
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
     const int hr = (tid >> 2) + 64 * k;
     const int hy = hr / HC;
-    hyx[k] = hr < HROWS ? hy * 64 + (hr - hy * HC) : 63 * 64;
+    hyx[k] = hr < HROWS ? hy * 64 + (hr - hy * HC) : 1 << 26;
   }
   int hpix[VPT];
   int spix = 0;  // shortcut tile: pixel of this thread's vector r = 0 (vector r: + 2 r W)
   auto halo_geom = [&](int b, int h0, int w0) {
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
-      const int ih = h0 + (hyx[k] >> 6) - 1, iw = w0 + (hyx[k] & 63) - 1;
+      const int ih = h0 + (hyx[k] >> 6) - 1, iw = w0 + (hyx[k] & 63) - 1;  // (past the halo: ih >= 2^20 > H)
       const bool ok = ((unsigned)ih < (unsigned)H) & ((unsigned)iw < (unsigned)W);
       hpix[k] = ok ? (b * H + ih) * W + iw : -1;
     }
@@ -299,9 +284,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
   };
 
   f32x4 acc[16][4];
-  u32x4 wcur[4], wnext[4], wb[3][4];  // wb: WD = 2, tap t's fragments in wb[t % 3] (9 taps: a whole number of turns)
-  constexpr int WD = SC ? 1 : H10_WD;
-  constexpr bool EARLY = !SC && H10_EARLY;
+  u32x4 wcur[4], wnext[4];
 
   // ---- prologue: the first tile's group 0 (shortcut chunks + main chunk 0), synchronously
   int n0, bb, h0, w0;
@@ -317,11 +300,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
   for (int k = 0; k < VPT; ++k) prep_store(k);
 #pragma unroll
   for (int q = 0; q < (SC ? 2 * SCV : 0); ++q) sc_store(q);
-  if constexpr (WD == 1) wload(wnext, n0, pn > 0, 0, pn > 0 ? pu0 : 0);
-  if constexpr (WD == 2) {
-    wload(wb[0], n0, false, 0, 0);
-    wload(wb[1], n0, false, 1, 0);
-  }
+  wload(wnext, n0, pn > 0, 0, pn > 0 ? pu0 : 0);
   gc = 0;
 
   for (int t = t_begin; t < t_end; ++t) {
@@ -397,24 +376,14 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
       static_for<144>([&](auto ST) {
         constexpr int st = decltype(ST)::value, tap = st / 16, i = st % 16;
         if constexpr (i == 0) {
-          if constexpr (WD == 2) {  // (no register copies: a copy would wait for the load it copies)
-            if constexpr (tap + 2 <= 8) wload(wb[(tap + 2) % 3], n0, false, tap + 2, c);
-            else wload(wb[(tap + 2) % 3], nn0, false, tap - 7, nc);
-          } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) wcur[j] = wnext[j];
-            if constexpr (tap < 8) wload(wnext, n0, false, tap + 1, c);
-            else wload(wnext, nn0, nsc_next, 0, nc);
-          }
+          for (int j = 0; j < 4; ++j) wcur[j] = wnext[j];
+          if constexpr (tap < 8) wload(wnext, n0, false, tap + 1, c);
+          else wload(wnext, nn0, nsc_next, 0, nc);
         }
         if constexpr (i + 4 < 16) hread(tap, i + 4);
         else if constexpr (tap < 8) hread(tap + 1, i - 12);
-        if constexpr (EARLY) {
-          if constexpr (st >= 1 && st <= 4) {
-#pragma unroll
-            for (int k = 3 * (st - 1); k < 3 * st && k < VPT; ++k) prep_load(k);
-          }
-        } else if constexpr (st >= LOAD0 && (st - LOAD0) % STRIDE == 0 && (st - LOAD0) / STRIDE < VPT) {
+        if constexpr (st >= LOAD0 && (st - LOAD0) % STRIDE == 0 && (st - LOAD0) / STRIDE < VPT) {
           prep_load((st - LOAD0) / STRIDE);
         }
         if constexpr (SC && st >= SCL0 && (st - SCL0) % SCSTRIDE == 0 && (st - SCL0) / SCSTRIDE < 2 * SCV) {
@@ -424,8 +393,7 @@ __global__ __launch_bounds__(256, 1) void conv_halo10_kernel(ConvParams p, int n
           constexpr int j = decltype(J)::value;
           if constexpr (i == 0 && j == 0)  // 2 wait states after any compiler VALU write of an operand (a copy)
             asm volatile("s_nop 1" ::: "memory");
-          if constexpr (WD == 2) a_mfma(acc[i][j], wb[tap % 3][j], hf[tap][i]);
-          else a_mfma(acc[i][j], wcur[j], hf[tap][i]);
+          a_mfma(acc[i][j], wcur[j], hf[tap][i]);
           xf_slice(ST, J);
         });
         if constexpr (st >= XF0 + NSLOT - 1 && (st - XF0 - NSLOT + 1) % STRIDE == 0 &&

@@ -71,6 +71,23 @@ def _compile(src: str, obj: str, extra=()):
     return obj
 
 
+def _read(path: str):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _obj_key(src: str, common: str, extra=()) -> str:
+    """Content key of one object: its source, the shared headers + build script (`common`) and its flags."""
+    h = hashlib.sha256(common.encode())
+    h.update(" ".join([*FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), *extra]).encode())
+    with open(src, "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()
+
+
 def build_library(force: bool = False, jobs: int = 8, extra_flags=(), lib: str = LIB, csrc: str = CSRC) -> str:
     """Build `lib`.  `extra_flags` (e.g. -DSNRSE_STAMPS for the timing-diagnostic build) go to
     every compile; such builds use their own object directory next to `lib`.  `csrc` selects another
@@ -82,20 +99,29 @@ def build_library(force: bool = False, jobs: int = 8, extra_flags=(), lib: str =
     t0 = time.time()
     objdir = os.path.join(os.path.dirname(lib), "obj")
     os.makedirs(objdir, exist_ok=True)
-    hdr_t = max([os.path.getmtime(h) for h in _headers(csrc) + [os.path.abspath(__file__)]] + [0.0])
+    # objects are reused only when their recorded key -- sha256 of the source, every header, this script and the
+    # compile flags, by content -- matches, so the linked objects are the tree's (an mtime-preserving copy of an old
+    # object is recompiled); abi.cpp carries the build id and is always recompiled
+    common = hashlib.sha256()
+    for f in sorted(_headers(csrc), key=os.path.basename) + [os.path.abspath(__file__)]:
+        common.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            common.update(fh.read())
     todo, objs = [], []
     for src in _sources(csrc):
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
         objs.append(obj)
-        if (force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_t)
-                or os.path.basename(src) == "abi.cpp"):  # abi.cpp carries the build id: always recompiled
-            todo.append((src, obj))
+        key = _obj_key(src, common.hexdigest(), tuple(extra_flags))
+        if force or os.path.basename(src) == "abi.cpp" or _read(obj + ".id") != key or not os.path.exists(obj):
+            todo.append((src, obj, key))
     idflag = (f'-DSNRSE_BUILD_ID="{bid}"',)
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo) or 1))) as ex:
-        futs = [ex.submit(_compile, s, o, tuple(extra_flags) + (idflag if os.path.basename(s) == "abi.cpp" else ()))
-                for s, o in todo]
-        for f in futs:
+        futs = [(ex.submit(_compile, s, o, tuple(extra_flags) + (idflag if os.path.basename(s) == "abi.cpp" else ())),
+                 o, k) for s, o, k in todo]
+        for f, o, k in futs:
             f.result()
+            with open(o + ".id", "w") as fh:
+                fh.write(k + "\n")
     tmp = lib + ".tmp"
     r = subprocess.run([HIPCC, "-shared", f"--offload-arch={ARCH}", *objs, "-o", tmp],
                        capture_output=True, text=True)
