@@ -19,6 +19,7 @@ CPU oracle: no GPU).  Prints ONE JSON line (rank 0).  See DESIGN.md §4 for the 
 from __future__ import annotations
 
 import argparse
+import ctypes
 import glob
 import json
 import math
@@ -109,7 +110,21 @@ def cpu_model():
     return "unknown"
 
 
+def _stable_malloc():
+    """glibc serves the oracle's large activations (> the adaptive mmap threshold, at most 32 MB) by fresh mmaps,
+    page-faulted on every NFE, while smaller ones move to the heap as the threshold adapts, so the NFE time drifts
+    over a run (round 5, profiles/r05c_cpu_full_n30.json: 2.2-2.4 s for the first NFEs, 1.4-1.9 s for the last).
+    All allocations from the heap, never trimmed: steady NFE times, and the sample extrapolates the full run."""
+    try:
+        libc = ctypes.CDLL("libc.so.6")
+        libc.mallopt(-4, 0)          # M_MMAP_MAX: no mmapped chunks
+        libc.mallopt(-1, 1 << 30)    # M_TRIM_THRESHOLD: keep freed heap memory
+    except (OSError, AttributeError):
+        pass
+
+
 def _cpu_env():
+    _stable_malloc()
     threads = cpu_threads()
     torch.set_num_threads(threads)
     return {"cores": threads, "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count()}
@@ -121,13 +136,15 @@ def _complex_noise(gen):
     return noise
 
 
-def cpu_baseline(seconds=4.0, n_steps=2, full=False, N=30):
+def cpu_baseline(seconds=4.0, n_steps=4, full=False, N=30, warm=2):
     """The oracle (CPU restatement of the reference path, pinned to the reference goldens) on the
     host: one synthetic `seconds` clip, STFT + exponent transform -> prior -> `n_steps` PC steps with
     the reference's reverse_diffusion + ALD algebra (sde_ref.pc_sample: 2 fp32 NCSN++ NFEs per step)
     -> spec_back + iSTFT.  The per-NFE time (step algebra included) is extrapolated to N steps
     (2N NFE).  full=True also runs the whole N=30 utterance once and reports it beside the
-    extrapolation."""
+    extrapolation.  `warm` untimed NFEs first: the first evaluations of a process run slower (allocator and
+    oneDNN primitive caches; round 4's single warm-up NFE left the extrapolation 1.3x the full run's per-NFE
+    time, profiles/r04b_cpu_full_n30.json); each timed NFE's duration is in the record."""
     from oracle import ncsnpp_ref, sde_ref, spec_ref
     env = _cpu_env()
     sd = ncsnpp_ref.state_dict_to_torch({k: v.numpy() for k, v in formula_weights().items()})
@@ -136,8 +153,13 @@ def cpu_baseline(seconds=4.0, n_steps=2, full=False, N=30):
     noise = _complex_noise(gen)
     sde = sde_ref.OUVE(theta=1.5, sigma_min=0.05, sigma_max=0.5, N=30)
 
+    nfe_times = []
+
     def score_fn(x, t, Y):  # ScoreModel.forward, model_type 'bbed' (model.py:488-489)
-        return -ncsnpp_ref.ncsnpp_forward(torch.cat([x, Y], 1), torch.full((x.shape[0],), float(t)), sd)
+        t0 = time.perf_counter()
+        out = -ncsnpp_ref.ncsnpp_forward(torch.cat([x, Y], 1), torch.full((x.shape[0],), float(t)), sd)
+        nfe_times.append(time.perf_counter() - t0)
+        return out
 
     def front():
         nf = np.abs(y).max()
@@ -151,7 +173,9 @@ def cpu_baseline(seconds=4.0, n_steps=2, full=False, N=30):
         t0 = time.perf_counter()
         Y, nf = front()
         t_front = time.perf_counter() - t0
-        score_fn(Y, 0.5, Y)  # warm-up NFE (allocator, oneDNN primitive cache)
+        for _ in range(warm):  # warm-up NFEs (allocator, oneDNN primitive cache)
+            score_fn(Y, 0.5, Y)
+        nfe_times.clear()
         t0 = time.perf_counter()
         x, nfe = sde_ref.pc_sample(sde, score_fn, Y, noise, N=n_steps, eps=0.03, snr=0.5)
         t_loop = time.perf_counter() - t0
@@ -165,15 +189,19 @@ def cpu_baseline(seconds=4.0, n_steps=2, full=False, N=30):
                           f"transform, {n_steps} reverse_diffusion+ALD PC steps ({nfe} NCSN++ NFEs at "
                           f"[1,2,256,{Y.shape[-1]}] with the reference step algebra) + iSTFT; {t_nfe:.2f} s/NFE "
                           f"extrapolated to N={N} ({2 * N} NFE/utt)"),
-               "s_per_nfe": t_nfe, "cpu_model": env["cpu_model"], "os_cpu_count": env["os_cpu_count"]}
+               "s_per_nfe": t_nfe, "nfe_seconds": [round(v, 3) for v in nfe_times], "warmup_nfe": warm,
+               "cpu_model": env["cpu_model"], "os_cpu_count": env["os_cpu_count"]}
         if full:
+            nfe_times.clear()
             t0 = time.perf_counter()
             Y, nf = front()
             x, nfe_full = sde_ref.pc_sample(sde, score_fn, Y, noise, N=30, eps=0.03, snr=0.5)
             back(x, nf)
             t_full = time.perf_counter() - t0
             res["full_utterance"] = {"N": 30, "nfe": nfe_full, "seconds": t_full, "utt_per_s": 1.0 / t_full,
-                                     "extrapolated_seconds": t_utt, "measured_over_extrapolated": t_full / t_utt}
+                                     "extrapolated_seconds": t_utt, "measured_over_extrapolated": t_full / t_utt,
+                                     "nfe_seconds_mean": sum(nfe_times) / len(nfe_times),
+                                     "nfe_seconds": [round(v, 3) for v in nfe_times]}
     return res
 
 
@@ -651,7 +679,7 @@ def run(args):
         if val is not None:
             cpu["validation"] = val
     elif rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c5":
-        cpu = cpu_baseline(seconds=args.seconds, n_steps=1, N=args.N)  # 2 NFEs of a 30 s clip
+        cpu = cpu_baseline(seconds=args.seconds, n_steps=1, N=args.N, warm=1)  # 2 NFEs of a 30 s clip
     elif rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c4":
         cpu = cpu_baseline_c4(seconds=args.seconds)
 

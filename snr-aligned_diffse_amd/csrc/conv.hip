@@ -1379,7 +1379,16 @@ SNRSE_DEV int h5_opaque(int v) {
   return r;
 }
 
-template <typename TO, int GNM, int EF, int TW>
+// SCD: the fused 1x1 shortcut's chunks run as LDS-DMA phases interleaved with the main chunks (round 5): a shortcut
+// phase stages its 128 x 32 weights AND its unpadded 256-px x 32-channel input tile (8 + 16 KB = one ring slot) by
+// LDS-DMA, issued at the start of the phase before it like any weight phase, so the tile's HBM latency is covered by
+// that phase's MFMAs (3 taps where a main phase precedes it).  Main chunk c carries k = sb(c + 1) - sb(c) shortcut
+// phases (sb(c) = c Csc / Cin chunks): k = 0: M0 M1 M2 | 1: M0 M1 M2 S | 2: M0 M1 S M2 S | >= 3: M0 S M1 S M2 S S..;
+// the next chunk's halo is stored in the shortcut phase after M2 (which reads no halo), so that chunk boundary needs
+// no extra barrier.  (Round 4 ran the shortcut chunks after the main ones as one-tap chunks staged through registers
+// like a halo, whose HBM latency then had one tap of cover each: 3-6 % slower on every shortcut shape, +0.9 % on the
+// C2 line, profiles/r05b_h5_sc_*.)  SCD = the launch has a shortcut; without one the loop is the 3-phase chunk loop.
+template <typename TO, int GNM, int EF, int TW, bool SCD>
 __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   constexpr int TH = 256 / TW, HC = TW + 2;
   constexpr int RW = TH / 4;                // image rows per wave
@@ -1426,8 +1435,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   const int cbm = Cin / KT;
   const int Csc_all = p.Csc + p.Csc1;
   const int cbs = p.sc_src ? Csc_all / KT : 0;
-  const int ncb = cbm + cbs;
-  const int nq = 3 * cbm + cbs;
+  const int nq = 3 * cbm + cbs;  // phases: 3 per main chunk (3 taps each) + 1 per shortcut chunk
   const int K1 = 9 * Cin;
   const int hcol = tid & 3;  // this thread's 16-B chunk (8 channels) of its halo rows
 
@@ -1454,18 +1462,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
       hv[j] = __builtin_amdgcn_raw_buffer_load_b128(r_, voff_, 0, 0);                               \
     }                                                                                               \
   } while (0)
-  auto halo_load = [&](int c) {
-    if (c < cbm) {
-      const int ch = c * KT;
-      if (ch < p.C0) SNRSE_HALO5_LOADS(p.src0, p.bytes0, p.C0, ch);
-      else SNRSE_HALO5_LOADS(p.src1, p.bytes1, p.C1, ch - p.C0);
-      if constexpr (GNM > 0) {
-        if (tid < 16) gnv = *(const f32x4*)((tid < 8 ? p.gn_scale : p.gn_shift) + (size_t)bb * Cin + ch + (tid & 7) * 4);
-      }
-    } else {
-      const int ch = (c - cbm) * KT;
-      if (ch < p.Csc) SNRSE_HALO5_LOADS(p.sc_src, p.sc_bytes0, p.Csc, ch);
-      else SNRSE_HALO5_LOADS(p.sc_src1, p.sc_bytes1, p.Csc1, ch - p.Csc);
+  auto halo_load = [&](int c) {  // main chunk c (the shortcut's tiles go by LDS-DMA, SCD)
+    const int ch = c * KT;
+    if (ch < p.C0) SNRSE_HALO5_LOADS(p.src0, p.bytes0, p.C0, ch);
+    else SNRSE_HALO5_LOADS(p.src1, p.bytes1, p.C1, ch - p.C0);
+    if constexpr (GNM > 0) {
+      if (tid < 16) gnv = *(const f32x4*)((tid < 8 ? p.gn_scale : p.gn_shift) + (size_t)bb * Cin + ch + (tid & 7) * 4);
     }
   };
 #undef SNRSE_HALO5_LOADS
@@ -1479,7 +1481,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
     }
   };
   auto halo_store = [&](int c) {
-    const bool tr = GNM > 0 && c < cbm;
+    const bool tr = GNM > 0;
     float gsc[8], gsh[8];
     if constexpr (GNM > 0) {
       if (tr) {
@@ -1500,28 +1502,44 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
       *(u32x4*)(halo + swz64(hr, hcol)) = v;
     }
   };
-  // weights of phase q -> ring slot q & 1: nt taps x 8 pieces of 1 KB (16 rows x 64 B), lane-
-  // linear LDS destination, swizzle applied on the source chunk.
-  auto wload = [&](int q) {
-    int c, t0, nt;
-    if (q < 3 * cbm) { c = q / 3; t0 = (q - c * 3) * 3; nt = 3; }
-    else { c = cbm + (q - 3 * cbm); t0 = 4; nt = 1; }
-    const bool mainw = c < cbm;
-    const int wld = mainw ? K1 : Csc_all;
-    const int kb = mainw ? c * KT : (c - cbm) * KT;
-    const __amdgpu_buffer_rsrc_t r = mainw ? make_rsrc(p.wgt, p.wbytes) : make_rsrc(p.sc_wgt, p.sc_wbytes);
-    char* dst = ring + (q & 1) * SLOT;
+  // LDS-DMA of a phase into ring slot dst: main (c, tap group g) = 3 weight taps; shortcut u = its weight tap
+  // (8 KB) + its input tile (16 KB, tile row r = pixel (r / TW, r % TW), 64-B rows, chunk swizzle on the source)
+  auto dma = [&](int c, int g, int u, char* dst) {
     const int rl = lane >> 2, sl = lane & 3;
-    for (int ii = wid; ii < nt * 8; ii += 4) {
-      const int jt = ii >> 3, pc = ii & 7;
-      const int koff = mainw ? (t0 + jt) * Cin + kb : kb;
-      const int row = pc * 16 + rl;
-      const unsigned voff = (unsigned)(((n0 + row) * wld + koff + (sl ^ ((row >> 1) & 3)) * 8) * 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          r, (__attribute__((address_space(3))) void*)(dst + jt * TAPB + pc * 1024), 16, voff, 0, 0, 0);
+    if (g < 3) {
+      const __amdgpu_buffer_rsrc_t r = make_rsrc(p.wgt, p.wbytes);
+      const int kb = c * KT;
+      for (int ii = wid; ii < 24; ii += 4) {
+        const int jt = ii >> 3, pc = ii & 7;
+        const int row = pc * 16 + rl;
+        const unsigned voff = (unsigned)(((n0 + row) * K1 + (3 * g + jt) * Cin + kb + (sl ^ ((row >> 1) & 3)) * 8) * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            r, (__attribute__((address_space(3))) void*)(dst + jt * TAPB + pc * 1024), 16, voff, 0, 0, 0);
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t r = make_rsrc(p.sc_wgt, p.sc_wbytes);
+      const int kb = u * KT;
+      for (int pc = wid; pc < 8; pc += 4) {
+        const int row = pc * 16 + rl;
+        const unsigned voff = (unsigned)(((n0 + row) * Csc_all + kb + (sl ^ ((row >> 1) & 3)) * 8) * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            r, (__attribute__((address_space(3))) void*)(dst + pc * 1024), 16, voff, 0, 0, 0);
+      }
+      const bool one = kb >= p.Csc;
+      const __amdgpu_buffer_rsrc_t rx = one ? make_rsrc(p.sc_src1, p.sc_bytes1) : make_rsrc(p.sc_src, p.sc_bytes0);
+      const int cs = one ? p.Csc1 : p.Csc, cb = one ? kb - p.Csc : kb;
+      const int pix0 = (bb * p.H + h0) * p.W + w0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int pc = wid + 4 * k;
+        const int row = pc * 16 + rl;
+        const int pix = pix0 + (row / TW) * p.W + row % TW;
+        const unsigned voff = (unsigned)((pix * cs + cb + (sl ^ ((row >> 1) & 3)) * 8) * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rx, (__attribute__((address_space(3))) void*)(dst + TAPB + pc * 1024), 16, voff, 0, 0, 0);
+      }
     }
   };
-
   f32x4 acc[2][4][4];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -1529,36 +1547,135 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int lrow = lane & 15, lg = lane >> 4;
 
+
+  if constexpr (SCD) {
+    // ---- main chunks with their shortcut phases interleaved (see the kernel comment) ----
+    auto nsc = [&](int c) { return (c + 1) * cbs / cbm - c * cbs / cbm; };
+    // kind of position s of a chunk with k shortcut phases: 0..2 = main tap group t0 = 3 kind, 3 = shortcut (su: its
+    // ordinal in the chunk)
+    auto kind_of = [](int s, int k, int& su) -> int {
+      su = 0;
+      if (k >= 3) {
+        if (s == 0 || s == 2 || s == 4) return s >> 1;
+        su = s <= 3 ? s >> 1 : s - 3;
+        return 3;
+      }
+      if (s < 2) return s;
+      if (k == 0) return 2;
+      if (k == 1) {
+        if (s == 2) return 2;
+        return 3;
+      }
+      if (s == 3) return 2;
+      su = s == 2 ? 0 : 1;
+      return 3;
+    };
+    auto m2_pos = [](int k) { return k >= 3 ? 4 : k == 2 ? 3 : 2; };  // position of M2
+    halo_load(0);
+    dma(0, 0, 0, ring);
+    if constexpr (GNM > 0) {
+      gn_publish();
+      __syncthreads();
+    }
+    halo_store(0);
+    // halo loads issued after a phase's DMA: each thread's HJ vectors (+ wave 0's GroupNorm affine load)
+    const bool w0g = GNM > 0 && wid == 0;
+    bool halo_inflight = false;
+    int c = 0, pos = 0, k = nsc(0), ub = 0;  // current phase: chunk c, position pos; ub = sb(c)
+    for (int q = 0; q < nq; ++q) {
+      int su;
+      const int kind = kind_of(pos, k, su);
+      // the next phase
+      int c2 = c, pos2 = pos + 1, k2 = k, ub2 = ub;
+      if (pos2 == 3 + k) { c2 = c + 1; pos2 = 0; ub2 = ub + k; k2 = c2 < cbm ? nsc(c2) : 0; }
+      int su2;
+      const int kind2 = kind_of(pos2, k2, su2);
+      if (halo_inflight) {
+        if (w0g) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(HJ + 1) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(HJ) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      if (q + 1 < nq) dma(c2, kind2, ub2 + su2, ring + ((q + 1) & 1) * SLOT);
+      halo_inflight = false;
+      if (kind == 0 && c + 1 < cbm) {
+        halo_load(c + 1);
+        halo_inflight = true;
+      }
+      // one MFMA code path for both kinds (two would double-allocate the accumulators): a main phase reads its 3 taps'
+      // A fragments from the halo (row stride HC), a shortcut phase its one tap from the slot's input tile (stride TW)
+      const char* sl = ring + (q & 1) * SLOT;
+      const bool mainph = kind < 3;
+      const char* abuf = mainph ? halo : sl + TAPB;
+      const int ntap = mainph ? 3 : 1, rs = mainph ? HC : TW;
+      for (int jt = 0; jt < ntap; ++jt) {
+        const int tp = 3 * kind + jt;
+        const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
+        const int arow = mainph ? (wid * RW + dy + 1) * HC + dx + 1 + lrow : wid * RW * TW + lrow;
+        const char* sb = sl + jt * TAPB;
+        u32x4 af[4], bfr[8];
+        // fragment i: pixels 16 i .. 16 i + 15 of the wave's 64 = image row (16 i) / TW, column (16 i) % TW
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = *(const u32x4*)(abuf + swz64(arow + (16 * i / TW) * rs + (16 * i) % TW, lg));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bfr[j] = *(const u32x4*)(sb + swz64(j * 16 + lrow, lg));
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[h][i][j] = mfma_chunk<bf16_t>(af[i], bfr[h * 4 + j], acc[h][i][j]);
+      }
+      if (c + 1 < cbm) {
+        if (kind == 2) {
+          gn_publish();  // the next chunk's GroupNorm affine, read by halo_store after the next barrier
+          if (k == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();  // every wave is done reading halo(c)
+            halo_store(c + 1);
+          }
+        } else if (kind == 3 && pos == m2_pos(k) + 1) {
+          halo_store(c + 1);  // the first shortcut phase after M2: no wave reads the halo here
+        }
+      }
+      c = c2; pos = pos2; k = k2; ub = ub2;
+    }
+  } else {
+  // no shortcut: 3 phases of 3 taps per chunk, the next chunk's halo stored behind one more barrier
   halo_load(0);
-  wload(0);
+  dma(0, 0, 0, ring);
   if constexpr (GNM > 0) {
     gn_publish();
     __syncthreads();
   }
   halo_store(0);
   SNRSE_STAMP(1);
-  const int lrow = lane & 15, lg = lane >> 4;
   bool halo_inflight = false;
+  const bool w0g = GNM > 0 && wid == 0;
   for (int q = 0; q < nq; ++q) {
-    int c, t0, nt;
-    if (q < 3 * cbm) { c = q / 3; t0 = (q - c * 3) * 3; nt = 3; }
-    else { c = cbm + (q - 3 * cbm); t0 = 4; nt = 1; }
-    const bool first = c < cbm ? t0 == 0 : true;
-    const bool last = c < cbm ? t0 == 6 : true;
-    // the halo prefetch issued after the previous phase's weights may stay in flight
-    if (halo_inflight) asm volatile("s_waitcnt vmcnt(7) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    const int c = q / 3, t0 = (q - c * 3) * 3;
+    const bool first = t0 == 0, last = t0 == 6;
+    // the halo prefetch issued after the previous phase's weights may stay in flight (HJ vectors + wave 0's
+    // GroupNorm affine load)
+    if (halo_inflight) {
+      if (w0g) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(HJ + 1) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(HJ) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     SNRSE_STAMP(2 + 2 * (q & 15));
-    if (q + 1 < nq) wload(q + 1);
+    if (q + 1 < nq) dma((q + 1) / 3, (q + 1) % 3, 0, ring + ((q + 1) & 1) * SLOT);
     halo_inflight = false;
-    if (first && c + 1 < ncb) {
+    if (first && c + 1 < cbm) {
       halo_load(c + 1);
       halo_inflight = !last && q + 1 < nq;
     }
     const char* sl = ring + (q & 1) * SLOT;
-    for (int jt = 0; jt < nt; ++jt) {
+    for (int jt = 0; jt < 3; ++jt) {
       const int tp = t0 + jt;
       const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
       const int hbase = (wid * RW + dy + 1) * HC + dx + 1 + lrow;
@@ -1578,12 +1695,13 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
             acc[h][i][j] = mfma_chunk<bf16_t>(af[i], bfr[h * 4 + j], acc[h][i][j]);  // D[px][co]
     }
     SNRSE_STAMP(3 + 2 * (q & 15));
-    if (last && c + 1 < ncb) {
+    if (last && c + 1 < cbm) {
       gn_publish();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave is done reading halo(c); chunk c+1's GN affine is in LDS
       halo_store(c + 1);
     }
+  }
   }
   SNRSE_STAMP(28);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1619,17 +1737,17 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 #endif
 }
 
-template <typename TO, int GNM, int EF, int TW>
+template <typename TO, int GNM, int EF, int TW, bool SCD>
 int launch_halo5_ef(ConvParams p, int grid, hipStream_t s) {
   // halo + weight ring + (stamps build: 4 x 32 stamps) + the next chunk's GroupNorm affine (2 x 32 f32),
   // and at least the epilogue's reuse of it: 4 waves' 64 x 68 f32 staging + the 4 x 128 x 2 f32 statistics
   constexpr size_t main_lds = (256 / TW + 2) * (TW + 2) * 64 + 2 * 3 * 128 * 64 + 1024 + 256;
   constexpr size_t epi_lds = 4 * (64 * 68 * 4) + 4 * 128 * 2 * 4;
   constexpr size_t lds = main_lds > epi_lds ? main_lds : epi_lds;
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_halo5_kernel<TO, GNM, EF, TW>,
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_halo5_kernel<TO, GNM, EF, TW, SCD>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   SNRSE_RET(attr);  // (thread-safe one-time set: a function-local static)
-  hipLaunchKernelGGL((conv_halo5_kernel<TO, GNM, EF, TW>), dim3(grid), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((conv_halo5_kernel<TO, GNM, EF, TW, SCD>), dim3(grid), dim3(256), lds, s, p);
   return (int)hipGetLastError();
 }
 
@@ -1643,27 +1761,39 @@ int launch_halo5_gn(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   cx.last_epi_nt = p.epi_nt;
   const int tiles = p.B * (p.H / (256 / TW)) * (p.W / TW) * p.ntn;
   const int grid = tiles;
+  const bool scd = p.sc_src != nullptr;  // the fused shortcut's chunks as LDS-DMA phases
   // the bf16 ResBlock configurations of the NCSN++ path get a branch-free epilogue (bias always on):
   // Conv_0 (+temb), Conv_1 (+residual | +1x1 shortcut as extra K | +Combine), each +-stats, +-NT
   if constexpr (sizeof(TO) == 2 && GNM != 1) {
     if (cx.h5_specialise && p.bias) {
-      switch (epi_flags(p)) {
 #define SNRSE_H5_EF(F) \
-  case (F): return launch_halo5_ef<TO, GNM, (F), TW>(p, grid, s);
-        SNRSE_H5_EF(EF_TEMB | EF_STATS)
-        SNRSE_H5_EF(EF_TEMB | EF_STATS | EF_NT)
-        SNRSE_H5_EF(EF_RES | EF_STATS)
-        SNRSE_H5_EF(EF_RES | EF_STATS | EF_NT)
-        SNRSE_H5_EF(EF_STATS)
-        SNRSE_H5_EF(EF_STATS | EF_NT)
-        SNRSE_H5_EF(EF_COMB | EF_STATS)
-        SNRSE_H5_EF(EF_TEMB)
-#undef SNRSE_H5_EF
-        default: break;
+  case (F): return launch_halo5_ef<TO, GNM, (F), TW, false>(p, grid, s);
+#define SNRSE_H5_EFS(F) \
+  case (F): return launch_halo5_ef<TO, GNM, (F), TW, true>(p, grid, s);
+      if (!scd) {
+        switch (epi_flags(p)) {
+          SNRSE_H5_EF(EF_TEMB | EF_STATS)
+          SNRSE_H5_EF(EF_TEMB | EF_STATS | EF_NT)
+          SNRSE_H5_EF(EF_RES | EF_STATS)
+          SNRSE_H5_EF(EF_RES | EF_STATS | EF_NT)
+          SNRSE_H5_EF(EF_STATS)
+          SNRSE_H5_EF(EF_STATS | EF_NT)
+          SNRSE_H5_EF(EF_TEMB)
+          default: break;
+        }
+      } else {  // Conv_1 with the fused Conv_2 shortcut (no residual), and the down-sampling block's + Combine
+        switch (epi_flags(p)) {
+          SNRSE_H5_EFS(EF_STATS)
+          SNRSE_H5_EFS(EF_STATS | EF_NT)
+          SNRSE_H5_EFS(EF_COMB | EF_STATS)
+          default: break;
+        }
       }
+#undef SNRSE_H5_EF
+#undef SNRSE_H5_EFS
     }
   }
-  return launch_halo5_ef<TO, GNM, EF_RT, TW>(p, grid, s);
+  return scd ? launch_halo5_ef<TO, GNM, EF_RT, TW, true>(p, grid, s) : launch_halo5_ef<TO, GNM, EF_RT, TW, false>(p, grid, s);
 }
 
 // GroupNorm prologue mode and tile width as template arguments: the halo transform is straight-line

@@ -442,12 +442,16 @@ def test_conv_fused_groupnorm_silu(gpu, shape, variant):
     (8, 256, 0, 256, 64, 128, 0, 0, True, True, False, True),      # two Cout tiles per image
     (2, 256, 256, 256, 32, 64, 0, 0, False, False, True, False),   # cat input, no GN
     (4, 256, 256, 256, 16, 64, 256, 256, True, False, False, True),  # up-path Conv_1 + cat shortcut, 256 ch
+    (2, 128, 0, 128, 64, 128, 256, 128, True, False, False, True),  # shortcut 3x the input (3 per main chunk)
+    (2, 256, 0, 256, 32, 64, 128, 0, True, False, False, True),    # shortcut half the input (0 / 1 per chunk)
+    (2, 64, 0, 128, 32, 64, 320, 0, True, False, False, True),     # 5 shortcut chunks per main chunk
 ])
 @pytest.mark.parametrize("tw", [0, 64])
 def test_conv_halo_large(gpu, case, tw):
     """The halo GEMM (v5, both tiles: 8 x 32 auto where H % 8 == 0, 4 x 64 forced) vs an fp32 torch
     reference on the GPU at multi-image sizes, with the fused GroupNorm+SiLU prologue, cat inputs, the
-    1x1 shortcut, temb, residual and the per-channel output statistics."""
+    1x1 shortcut (its chunks as LDS-DMA phases between the main ones: 0 / 1 / 2 / 3 / 5 per main chunk), temb,
+    residual and the per-channel output statistics."""
     variant = 5
     from snrse import ops
     B, C0, C1, Co, H, W, Csc, Csc1, use_gn, use_temb, use_res, use_st = case

@@ -24,6 +24,9 @@ SHAPES = [
     (32, 256, 0, 768, 16, 32, 1, 0),
     (32, 128, 0, 128, 256, 512, 3, 256),   # 7: up-path Conv_1 at level 0: shortcut over cat(h, skip) = 256 channels
     (32, 256, 0, 256, 128, 256, 3, 512),   # 8: the same at level 1
+    (32, 128, 0, 128, 128, 256, 3, 256),   # 9: level-1 up-path Conv_1 (RB 67-68: 128 couts, cat shortcut)
+    (32, 256, 0, 256, 128, 256, 3, 256),   # 10: RB 65 Conv_1 (up-sampling block: FIR'd shortcut, Csc = Cin)
+    (32, 256, 0, 256, 64, 128, 3, 512),    # 11: level-2 up-path Conv_1 (RB 60-61)
 ]
 
 
@@ -35,7 +38,7 @@ def _gn_pair(B, C, dev, g):
     return ss[0], ss[1]
 
 
-def run(shape, variant, reps, dev, gn=False):
+def run(shape, variant, reps, dev, gn=False, opt=None):
     B, C0, C1, Co, H, W, k, Csc = shape
     g = torch.Generator(device=dev).manual_seed(0)
     x0 = torch.randn(B, H, W, C0, device=dev, generator=g).bfloat16()
@@ -48,7 +51,10 @@ def run(shape, variant, reps, dev, gn=False):
     gnp = None
     if gn and k == 3:
         gnp = _gn_pair(B, C0 + C1, dev, g)
-    ops.set_option("conv_variant", variant)
+    if opt:
+        ops.set_option(opt[0], opt[1])
+    else:
+        ops.set_option("conv_variant", variant)
     out = ops.conv2d(x0, w, k, Co, bias=bias, src1=x1, sc=sc, sc_wgt=ws, stats=st, gn=gnp)
     torch.cuda.synchronize()
     ts = []
@@ -71,6 +77,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--shapes", default="", help="comma list of SHAPES indices (default all)")
     ap.add_argument("--gn", action="store_true", help="fused GroupNorm+SiLU prologue (halo kernels)")
+    ap.add_argument("--option", default="", help="A/B an option instead of conv_variant: --variants are its values")
     a = ap.parse_args()
     dev = torch.device("cuda")
     res = []
@@ -80,7 +87,7 @@ def main():
         row = {"shape": sh}
         for rnd in range(a.rounds):  # interleaved A/B rounds: clocks drift between launches
             for v in [int(x) for x in a.variants.split(",")]:
-                out, ms, fl = run(sh, v, a.reps, dev, gn=a.gn)
+                out, ms, fl = run(sh, v, a.reps, dev, gn=a.gn, opt=(a.option, v) if a.option else None)
                 outs[v] = out.float()
                 ms = min(ms, row.get(f"v{v}_ms", ms))
                 row[f"v{v}_ms"] = ms
@@ -90,6 +97,8 @@ def main():
             d = (outs[ks[0]] - outs[ks[1]]).abs().max().item()
             row["max_abs_diff"] = d
         res.append(row)
+        if a.option:
+            row["option"] = a.option
         print(json.dumps(row), flush=True)
     ops.set_option("conv_variant", 0)
 
