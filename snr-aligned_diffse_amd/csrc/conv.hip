@@ -779,12 +779,13 @@ constexpr size_t LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
 }  // namespace x3h
 // the same geometry for tile width TW (64: 4 x 64 px, the namespace above; 32: 8 x 32 px, 340 halo rows per 256
 // pixels instead of 396 -- 14 % less halo to load, split and GroupNorm per output, as v5's 8 x 32 form)
-template <int TW_>
+template <int TW_, int SPR_ = 1>
 struct X3G {
   static constexpr int TW = TW_, TH = 256 / TW_, HC = TW_ + 2, HROWS = (TH + 2) * HC;
   static constexpr int HBYTES = HROWS * 128, HJ = (HROWS * 8 + 511) / 512, TAPB = x3h::TAPB;
   static constexpr int RW = 64 / TW_;  // image rows of a wave's 64 pixels
-  static constexpr size_t LDS_MAIN = 2 * (size_t)HBYTES + 3 * (size_t)TAPB;
+  // weight ring: 3 one-tap slots, or (SPR 2, the pair schedule) 2 two-tap slots
+  static constexpr size_t LDS_MAIN = 2 * (size_t)HBYTES + (SPR_ == 2 ? 4 : 3) * (size_t)TAPB;
   static constexpr size_t LDS = LDS_MAIN > x3h::LDS_EPI ? LDS_MAIN : x3h::LDS_EPI;
 };
 
@@ -802,9 +803,13 @@ SNRSE_DEV void x3h_vm_wait(int n) {
 
 // GNM: GroupNorm prologue of the main input as in the bf16 halo kernel (0 none, 1 affine, 2 affine +
 // SiLU), applied once per halo element while it is split: the fp32 mode's gn_act pass disappears.
-template <int GNM, bool SPR, int TWV>
+// SPR: 0 one phase per tap, the next chunk's halo stored in one go; 1 the same, stored one piece per tap; 2 (round 5,
+// the pair schedule: TW 32, an even number of main chunks) TWO taps per phase -- half the barriers -- over a 2-slot
+// ring of 2-tap weight slots, the main chunks in pairs (18 taps = 9 phases with compile-time taps), the next chunk's
+// halo pieces stored after its taps 2..7
+template <int GNM, int SPR, int TWV>
 __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
-  using G = X3G<TWV>;
+  using G = X3G<TWV, SPR>;
   constexpr int TH = G::TH, TW = G::TW, HC = G::HC, HROWS = G::HROWS, HBYTES = G::HBYTES, HJ = G::HJ;
   constexpr int TAPB = G::TAPB, RW = G::RW;
   constexpr int HOPS = HJ + (GNM > 0 ? 2 : 0);  // vector-memory ops of one halo prefetch per thread
@@ -864,6 +869,9 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
 #pragma unroll
     for (int j = 0; j < HJ; ++j) {
       const int voff = hok[j] ? (hpix[j] * cs + cc + hch * 4) * 4 : (int)0x80000000;  // outside: zero padding
+#ifdef X3H_EXP_NOHALO  // timing diagnostics only (results wrong): no halo loads after the first chunk
+      if (c > 0) { hv[j] = u32x4{(uint32_t)voff, 0u, 0u, 0u}; continue; }
+#endif
       hv[j] = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
     }
     if constexpr (GNM > 0) {  // issued for shortcut chunks too (unused there): a fixed count per prefetch
@@ -909,6 +917,13 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
     float x[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) x[k] = __uint_as_float(hv[j][k]);
+#ifdef X3H_EXP_NOXF  // timing diagnostics only (results wrong): the halo stored without GroupNorm / split VALU
+    if (j < HJ - 1 || hr < HROWS) {
+      *(u32x2*)(hb + swz(hr, hch >> 1) + (hch & 1) * 8) = u32x2{hv[j][0], hv[j][1]};
+      *(u32x2*)(hb + swz(hr, 4 + (hch >> 1)) + (hch & 1) * 8) = u32x2{hv[j][2], hv[j][3]};
+    }
+    return;
+#endif
     if constexpr (GNM > 0) {
       const uint32_t keep = tr ? 0u : ~0u, zero = (hok[j] || !tr) ? ~0u : 0u;
 #pragma unroll
@@ -962,8 +977,29 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  wload(0);
-  if (nq > 1) wload(1);
+  // one tap's weights (chunk c, tap tp) -> dst: 16 pieces of 1 KB, 2 per wave (the pair schedule's DMA)
+  auto wtap = [&](int c, int tp, char* dst) {
+    const bool mainw = c < cbm;
+    const int wld = mainw ? 2 * K1 : 2 * Csc_all;
+    const int koff = mainw ? 2 * (tp * Cin + c * 32) : 2 * ((c - cbm) * 32);
+    const __amdgpu_buffer_rsrc_t r = mainw ? make_rsrc(p.wgt, p.wbytes) : make_rsrc(p.sc_wgt, p.sc_wbytes);
+    const int rl = lane >> 3, sl = lane & 7;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int pc = wid * 2 + k;
+      const int row = pc * 8 + rl;
+      const unsigned voff = (unsigned)(((n0 + row) * wld + koff + (sl ^ (row & 7)) * 8) * 2);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(dst + pc * 1024), 16,
+                                               voff, 0, 0, 0);
+    }
+  };
+  if constexpr (SPR == 2) {
+    wtap(0, 0, ring);
+    wtap(0, 1, ring + TAPB);
+  } else {
+    wload(0);
+    if (nq > 1) wload(1);
+  }
   halo_load(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   halo_store(0);
@@ -994,7 +1030,90 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
         acc[i][j] = mfma_chunk<bf16_t>(al[i], bh[j], acc[i][j]);
       }
   };
-  if constexpr (SPR) {
+  if constexpr (SPR == 2) {
+    // The pair schedule.  Phase k of a chunk pair (c0, c1 = c0 + 1) runs taps s = 2k, 2k + 1 of the pair's 18
+    // (chunk c0 + s / 9, tap s % 9) from ring slot `so`; at its top it waits for its own DMA (issued at the top of
+    // phase k - 1; the halo prefetch issued behind that DMA at phase 0 / 4 may stay in flight), then issues the next
+    // phase's DMA.  The halo of chunk c + 1 is prefetched at the phase holding tap (c, 0) and stored, split (+
+    // GroupNorm), one piece after each of the taps (c, 2 .. 7) into the other halo buffer (HJ = 6 pieces at TW 32);
+    // the last piece lands a barrier before tap (c + 1, 0) is read.  Then the shortcut chunks, one tap per phase.
+    static_assert(TW == 32 && HJ == 6, "pair schedule: 8 x 32 tiles, 6 halo pieces per thread");
+    constexpr int SLOT2 = 2 * TAPB;
+    int so = 0;
+    auto wait_vm = [](int n) {  // vmcnt(n) for n in {0, HOPS} (compile-time encodings)
+      if (n == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(HOPS) : "memory");
+    };
+    for (int c0 = 0; c0 < cbm; c0 += 2) {
+      const int c1 = c0 + 1;
+      const bool more = c0 + 2 < cbm;        // another pair follows
+      const bool pf1 = more || cbs > 0;       // a chunk follows c1 (main or shortcut): prefetched at phase 4
+      bool infl = false;                       // halo loads issued behind the current phase's DMA
+      static_for<9>([&](auto K) {
+        constexpr int k = decltype(K)::value;
+        constexpr int sa = 2 * k, sb = 2 * k + 1;
+        constexpr int da = sa / 9, ta = sa % 9, db = sb / 9, tb = sb % 9;
+        wait_vm(infl ? HOPS : 0);
+        __builtin_amdgcn_s_barrier();
+        // the next phase's DMA into the other slot
+        char* const nxt = ring + (SLOT2 - so);
+        if constexpr (k < 8) {
+          wtap(c0 + (2 * k + 2) / 9, (2 * k + 2) % 9, nxt);
+          wtap(c0 + (2 * k + 3) / 9, (2 * k + 3) % 9, nxt + TAPB);
+        } else {
+          if (more) {
+            wtap(c0 + 2, 0, nxt);
+            wtap(c0 + 2, 1, nxt + TAPB);
+          } else if (cbs > 0) {
+            wtap(cbm, 4, nxt);
+          }
+        }
+        infl = false;
+        if constexpr (k == 0) {
+          halo_load(c1);
+          infl = true;
+        }
+        if constexpr (k == 4) {
+          if (pf1) {
+            halo_load(c1 + 1);
+            infl = true;
+          }
+        }
+        const char* const sl_ = ring + so;
+        // tap A, then its halo piece; tap B, then its piece.  Piece j of chunk c's successor after tap (c, 2 + j);
+        // before the first one (tap 2) the halo loads are waited for (only this phase's 4 DMA pieces are younger)
+        auto piece_after = [&](int d, int t) {
+          const int c = c0 + d;
+          if (t < 2 || t > 7) return;
+          if (d == 1 && !pf1) return;
+          if (t == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+          halo_piece(smem + ((c + 1) & 1) * HBYTES, t - 2, c + 1 < cbm);
+        };
+        tap_mfma(smem + ((c0 + da) & 1) * HBYTES, sl_, ta);
+        piece_after(da, ta);
+        __builtin_amdgcn_sched_barrier(0);  // one tap at a time (hoisted fragment reads of the next tap spill)
+        tap_mfma(smem + ((c0 + db) & 1) * HBYTES, sl_ + TAPB, tb);
+        piece_after(db, tb);
+        __builtin_amdgcn_sched_barrier(0);
+        so = SLOT2 - so;
+      });
+    }
+    // the shortcut chunks: one tap (the center) per phase; chunk cbm's halo was stored during the last pair
+    for (int c = cbm; c < ncb; ++c) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (c + 1 < ncb) wtap(c + 1, 4, ring + (SLOT2 - so));
+      if (c + 1 < ncb) halo_load(c + 1);
+      tap_mfma(smem + (c & 1) * HBYTES, ring + so, 4);
+      if (c + 1 < ncb) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        char* const nb_ = smem + ((c + 1) & 1) * HBYTES;
+#pragma unroll
+        for (int j = 0; j < HJ; ++j) halo_piece(nb_, j, false);
+      }
+      so = SLOT2 - so;
+    }
+  } else if constexpr (SPR == 1) {
     // Branch-free schedule: every phase issues its DMA two phases ahead (zero-filling past the end), every
     // chunk prefetches the next one's halo at its first phase (the last chunk re-reads itself into the
     // unused buffer), so the ops issued after DMA(q) are DMA(q+1) plus the halo prefetches of phases q-1 /
@@ -1012,6 +1131,9 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
         if (tp == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + HOPS) : "memory");
         else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifdef X3H_EXP_BAR3  // timing diagnostics only (results wrong): a barrier every third tap instead of every tap
+        if (tp % 3 == 0)
+#endif
         __builtin_amdgcn_s_barrier();
         wload(q + 2);
         if (tp == 0) halo_load(c + 1 < ncb ? c + 1 : c);
@@ -1081,6 +1203,9 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // LDS is reused as the epilogue staging area
+#ifdef X3H_EXP_NOEPI  // timing diagnostics: the epilogue exists but is skipped at run time (out_scale never equals this)
+  if (p.out_scale != 12345.f) return;
+#endif
   const int mb = (bb * p.H + h0 + wr * RW) * p.W + w0;
   if constexpr (TW == 64)
     epilogue_lds<float, 4, 128>(p, acc, mb, n0 + wc * 64, lane, (float*)(smem + wid * (64 * 68 * 4)),
@@ -1464,8 +1589,10 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   } while (0)
   auto halo_load = [&](int c) {  // main chunk c (the shortcut's tiles go by LDS-DMA, SCD)
     const int ch = c * KT;
-    if (ch < p.C0) SNRSE_HALO5_LOADS(p.src0, p.bytes0, p.C0, ch);
-    else SNRSE_HALO5_LOADS(p.src1, p.bytes1, p.C1, ch - p.C0);
+    // one load sequence with the source selected by scalars (two branches, each with its own loads, made the
+    // compiler's waitcnt model assume the other branch's loads pending: a vmcnt(0) on every src1 chunk)
+    const bool s1 = ch >= p.C0;
+    SNRSE_HALO5_LOADS(s1 ? p.src1 : p.src0, s1 ? p.bytes1 : p.bytes0, s1 ? p.C1 : p.C0, s1 ? ch - p.C0 : ch);
     if constexpr (GNM > 0) {
       if (tid < 16) gnv = *(const f32x4*)((tid < 8 ? p.gn_scale : p.gn_shift) + (size_t)bb * Cin + ch + (tid & 7) * 4);
     }
@@ -1504,24 +1631,32 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   };
   // LDS-DMA of a phase into ring slot dst: main (c, tap group g) = 3 weight taps; shortcut u = its weight tap
   // (8 KB) + its input tile (16 KB, tile row r = pixel (r / TW, r % TW), 64-B rows, chunk swizzle on the source)
-  auto dma = [&](int c, int g, int u, char* dst) {
+  // oob: the phase after the last one -- the same 6 pieces per wave, out of range (no memory access; zeros land in the
+  // free ring slot), so every phase issues a fixed count (vm_after_dma)
+  auto dma = [&](int c, int g, int u, char* dst, bool oob = false) {
     const int rl = lane >> 2, sl = lane & 3;
+    const unsigned oobm = oob ? 0x80000000u : 0u;
     if (g < 3) {
       const __amdgpu_buffer_rsrc_t r = make_rsrc(p.wgt, p.wbytes);
       const int kb = c * KT;
-      for (int ii = wid; ii < 24; ii += 4) {
+      // (a compile-time count per wave: 6 pieces, so the compiler's waitcnt model can count them -- vm_after_dma)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const int ii = wid + 4 * k;
         const int jt = ii >> 3, pc = ii & 7;
         const int row = pc * 16 + rl;
-        const unsigned voff = (unsigned)(((n0 + row) * K1 + (3 * g + jt) * Cin + kb + (sl ^ ((row >> 1) & 3)) * 8) * 2);
+        const unsigned voff = oobm | (unsigned)(((n0 + row) * K1 + (3 * g + jt) * Cin + kb + (sl ^ ((row >> 1) & 3)) * 8) * 2);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             r, (__attribute__((address_space(3))) void*)(dst + jt * TAPB + pc * 1024), 16, voff, 0, 0, 0);
       }
     } else {
       const __amdgpu_buffer_rsrc_t r = make_rsrc(p.sc_wgt, p.sc_wbytes);
       const int kb = u * KT;
-      for (int pc = wid; pc < 8; pc += 4) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int pc = wid + 4 * k;
         const int row = pc * 16 + rl;
-        const unsigned voff = (unsigned)(((n0 + row) * Csc_all + kb + (sl ^ ((row >> 1) & 3)) * 8) * 2);
+        const unsigned voff = oobm | (unsigned)(((n0 + row) * Csc_all + kb + (sl ^ ((row >> 1) & 3)) * 8) * 2);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             r, (__attribute__((address_space(3))) void*)(dst + pc * 1024), 16, voff, 0, 0, 0);
       }
@@ -1534,7 +1669,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
         const int pc = wid + 4 * k;
         const int row = pc * 16 + rl;
         const int pix = pix0 + (row / TW) * p.W + row % TW;
-        const unsigned voff = (unsigned)((pix * cs + cb + (sl ^ ((row >> 1) & 3)) * 8) * 2);
+        const unsigned voff = oobm | (unsigned)((pix * cs + cb + (sl ^ ((row >> 1) & 3)) * 8) * 2);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rx, (__attribute__((address_space(3))) void*)(dst + TAPB + pc * 1024), 16, voff, 0, 0, 0);
       }
@@ -1548,6 +1683,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int lrow = lane & 15, lg = lane >> 4;
+  // Where this is called, the phase's top already waited for every older vector-memory op and only the 6 LDS-DMA
+  // pieces this wave issued since may be in flight, so the wait returns at once.  It is for the compiler: its
+  // waitcnt model merges the loop's in-flight-halo path into every phase and would otherwise wait for those fresh
+  // DMA pieces (an L2 round trip) before re-filling or storing the halo registers (round 5: a vmcnt(0) after the
+  // DMA issue in every chunk's first phase, vmcnt(5..2) in the halo store).  A builtin, not asm: the model sees it.
+  auto vm_after_dma = [&]() { __builtin_amdgcn_s_waitcnt(0x0f76); };  // vmcnt(6) expcnt(7) lgkmcnt(15): no lgkm wait
 
 
   if constexpr (SCD) {
@@ -1599,9 +1740,10 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       }
       __builtin_amdgcn_s_barrier();
-      if (q + 1 < nq) dma(c2, kind2, ub2 + su2, ring + ((q + 1) & 1) * SLOT);
+      dma(c2 < cbm ? c2 : 0, kind2, ub2 + su2, ring + ((q + 1) & 1) * SLOT, q + 1 >= nq);
       halo_inflight = false;
       if (kind == 0 && c + 1 < cbm) {
+        vm_after_dma();
         halo_load(c + 1);
         halo_inflight = true;
       }
@@ -1635,9 +1777,11 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
           if (k == 0) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();  // every wave is done reading halo(c)
+            vm_after_dma();
             halo_store(c + 1);
           }
         } else if (kind == 3 && pos == m2_pos(k) + 1) {
+          vm_after_dma();
           halo_store(c + 1);  // the first shortcut phase after M2: no wave reads the halo here
         }
       }
@@ -1668,9 +1812,10 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
     }
     __builtin_amdgcn_s_barrier();
     SNRSE_STAMP(2 + 2 * (q & 15));
-    if (q + 1 < nq) dma((q + 1) / 3, (q + 1) % 3, 0, ring + ((q + 1) & 1) * SLOT);
+    dma(q + 1 < nq ? (q + 1) / 3 : 0, (q + 1) % 3, 0, ring + ((q + 1) & 1) * SLOT, q + 1 >= nq);
     halo_inflight = false;
     if (first && c + 1 < cbm) {
+      vm_after_dma();
       halo_load(c + 1);
       halo_inflight = !last && q + 1 < nq;
     }
@@ -1699,12 +1844,13 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
       gn_publish();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave is done reading halo(c); chunk c+1's GN affine is in LDS
+      vm_after_dma();
       halo_store(c + 1);
     }
   }
   }
   SNRSE_STAMP(28);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // (the out-of-range DMA after the last phase too)
   __builtin_amdgcn_s_barrier();  // LDS is reused as the epilogue staging area
   float* const stage = (float*)(smem + wid * (64 * 68 * 4));
   float* const red = (float*)(smem + 4 * (64 * 68 * 4));
@@ -1875,18 +2021,20 @@ int launch_x3(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   return (int)hipGetLastError();
 }
 
-template <int GNM, bool SPR, int TWV>
+template <int GNM, int SPR, int TWV>
 int launch_x3h_gn(ConvParams p, hipStream_t s, int tiles) {
   static const hipError_t attr = hipFuncSetAttribute((const void*)conv_x3h_kernel<GNM, SPR, TWV>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)X3G<TWV>::LDS);
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)X3G<TWV, SPR>::LDS);
   SNRSE_RET(attr);
   p.ntn = p.Cout / 128;
   p.ksplit = 1;
-  hipLaunchKernelGGL((conv_x3h_kernel<GNM, SPR, TWV>), dim3(tiles), dim3(512), X3G<TWV>::LDS, s, p);
+  constexpr size_t lds = X3G<TWV, SPR>::LDS;
+  hipLaunchKernelGGL((conv_x3h_kernel<GNM, SPR, TWV>), dim3(tiles), dim3(512), lds, s, p);
   return (int)hipGetLastError();
 }
 
-template <bool SPR, int TWV>
+template <int SPR, int TWV>
 int launch_x3h_spr(const ConvParams& p, hipStream_t s, int tiles) {
   if (!p.gn_scale) return launch_x3h_gn<0, SPR, TWV>(p, s, tiles);
   if (!p.gn_act) return launch_x3h_gn<1, SPR, TWV>(p, s, tiles);
@@ -1895,8 +2043,13 @@ int launch_x3h_spr(const ConvParams& p, hipStream_t s, int tiles) {
 
 // tw 32: the 8 x 32 px tiles (H % 8 == 0, W % 32 == 0; tiles counted for them), else 4 x 64
 int launch_x3h(const ConvParams& p, hipStream_t s, int tiles, int spread, int tw) {
-  if (tw == 32) return spread ? launch_x3h_spr<true, 32>(p, s, tiles) : launch_x3h_spr<false, 32>(p, s, tiles);
-  return spread ? launch_x3h_spr<true, 64>(p, s, tiles) : launch_x3h_spr<false, 64>(p, s, tiles);
+  // the pair schedule (spread 2) needs 8 x 32 tiles and an even number of 32-channel main chunks
+  if (spread == 2 && !(tw == 32 && ((p.C0 + p.C1) / 32) % 2 == 0)) spread = 1;
+  if (tw == 32) {
+    if (spread == 2) return launch_x3h_spr<2, 32>(p, s, tiles);
+    return spread ? launch_x3h_spr<1, 32>(p, s, tiles) : launch_x3h_spr<0, 32>(p, s, tiles);
+  }
+  return spread ? launch_x3h_spr<1, 64>(p, s, tiles) : launch_x3h_spr<0, 64>(p, s, tiles);
 }
 
 template <int BM, int BN, typename TO>

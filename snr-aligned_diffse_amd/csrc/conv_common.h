@@ -3,6 +3,9 @@
 #pragma once
 #include "common.h"
 
+#include <type_traits>
+#include <utility>
+
 namespace snrse_conv {
 
 template <typename T> struct ConvTraits;
@@ -81,6 +84,16 @@ SNRSE_DEV f32x4 mfma_chunk<float>(const u32x4& a, const u32x4& b, f32x4 acc) {
 }
 
 SNRSE_DEV int swz(int row, int chunk) { return (row << 7) + ((chunk ^ (row & 7)) << 4); }
+
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): compile-time step indices for hand-scheduled loops
+template <int N, typename F, int... S>
+SNRSE_DEV void static_for_impl(F&& f, std::integer_sequence<int, S...>) {
+  (f(std::integral_constant<int, S>{}), ...);
+}
+template <int N, typename F>
+SNRSE_DEV void static_for(F&& f) {
+  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
+}
 
 SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
   const uint64_t a = (uint64_t)base;

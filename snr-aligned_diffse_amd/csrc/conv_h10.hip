@@ -63,14 +63,6 @@ SNRSE_DEV uint32_t a_cvtpk(float a, float b) {
   return d;
 }
 SNRSE_DEV void a_and(uint32_t& d, uint32_t m) { asm volatile("v_and_b32 %0, %0, %1" : "+v"(d) : "v"(m)); }
-template <int N, typename F, int... S>
-SNRSE_DEV void static_for_impl(F&& f, std::integer_sequence<int, S...>) {
-  (f(std::integral_constant<int, S>{}), ...);
-}
-template <int N, typename F>
-SNRSE_DEV void static_for(F&& f) {
-  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
-}
 SNRSE_DEV void a_mfma(f32x4& acc, const u32x4& w, const u32x4& h) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(w), "v"(h));
 }

@@ -193,13 +193,15 @@ def test_x3_level0_vs_exact_fp32(gpu):
     assert rel(ops.fold_stats(st_b), ops.fold_stats(st_a)) < 1e-5
 
 
-@pytest.mark.parametrize("spread", [1, 0])
+@pytest.mark.parametrize("spread", [2, 1, 0])
 @pytest.mark.parametrize("act", [True, False])
 @pytest.mark.parametrize("shape", [(2, 128, 128, 8, 64), (1, 384, 256, 4, 128), (2, 256, 128, 4, 64),
-                                   (1, 128, 128, 8, 72)])
+                                   (1, 128, 128, 8, 72), (1, 384, 256, 8, 64), (1, 96, 128, 8, 32)])
 def test_x3h_fused_groupnorm_silu(gpu, shape, act, spread):
     """The halo form consuming SiLU(GN(x)) (act) or GN(x) from raw fp32 x + per-(b, c) scale / shift, with a
-    raw 1x1 shortcut as extra K; every other split conv rejects a fused GroupNorm."""
+    raw 1x1 shortcut as extra K; every other split conv rejects a fused GroupNorm.  spread 2 = the pair schedule
+    (two taps per phase) where its tiles apply (8 x 32, an even number of main chunks: the (2, 128, ...) and
+    (1, 384, 256, 8, 64) cases; the others fall back to spread 1)."""
     from snrse import ops
     B, cin, cout, H, W = shape
     x = torch.from_numpy(fnormal("t.fg.x", (B, cin, H, W))) * 1.5 + 0.2

@@ -39,11 +39,12 @@ def main():
     ap.add_argument("--exact", type=int, default=1)
     ap.add_argument("--gn", type=int, default=0, help="1: fused GroupNorm+SiLU on the x3h variants (x3_tile 0)")
     ap.add_argument("--spread", default="1", help="x3_spread settings to run each split variant with")
-    ap.add_argument("--h10", type=int, default=0, help="1: also the v10 split kernel (option h10), with --gn fused")
+    ap.add_argument("--shapes", default="", help="comma list of SHAPES indices (default all)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
-    for B, C0, C1, Co, H, W in SHAPES:
+    sel = [SHAPES[int(i)] for i in args.shapes.split(",")] if args.shapes else SHAPES
+    for B, C0, C1, Co, H, W in sel:
         x0 = torch.randn(B, H, W, C0, device=dev, generator=g)
         x1 = torch.randn(B, H, W, C1, device=dev, generator=g) if C1 else None
         w = torch.randn(Co, 9 * (C0 + C1), device=dev, generator=g) / math.sqrt(9 * (C0 + C1))
@@ -60,14 +61,10 @@ def main():
             sc = torch.rand(B, C0 + C1, device=dev, generator=g) + 0.5
             gn = (sc, torch.randn(B, C0 + C1, device=dev, generator=g) * 0.1)
             variants = [("x3gn", 0, sp) for sp in spreads] + variants
-        if args.h10:
-            variants = [("x3gn10" if args.gn else "x310", 0, 1)] + variants
         ref = None
-        h10_prev = ops.get_option("h10")
         for kind, t, sp in variants:
             ops.set_option("x3_tile", t)
             ops.set_option("x3_spread", sp)
-            ops.set_option("h10", 1 if kind.endswith("10") else 0)  # (x3 takes v10x3 only under h10 = 1)
             wt = w if kind == "exact" else ws
             kw = {"gn": gn} if kind.startswith("x3gn") else {}
             fn = lambda: ops.conv2d(x0, wt, 3, Co, bias=b, src1=x1, out=out, stats=st, **kw)  # noqa: E731
@@ -83,7 +80,6 @@ def main():
                               "ksplit": ops.get_option("last_ksplit"), "rel_vs_first": err}), flush=True)
         ops.set_option("x3_tile", 0)
         ops.set_option("x3_spread", 1)
-        ops.set_option("h10", h10_prev)
         del x0, x1, out, ref
 
 
