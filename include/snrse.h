@@ -168,7 +168,10 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  *   staged through LDS for whole-KB stores, 1 input rows only, 2 with the channels split over wave pairs, 0 the
  *   streaming form (all bit-identical but 2's statistics fold order);
  * "x3_tw" fp32x3 halo GEMM tile: 0 (default) 8 x 32 px where H % 8 == 0 and W % 32 == 0, else 4 x 64; 64 forces
- *   4 x 64; "x3_nt" 1 (default) its fp32 output stores non-temporal under the "epi_nt" rule. */
+ *   4 x 64; "x3_nt" 1 (default) its fp32 output stores non-temporal under the "epi_nt" rule;
+ * "x3_spread" fp32x3 halo GEMM schedule: 2 (default) two taps per barrier phase where its tiles are 8 x 32 px and the
+ *   main input has an even number of 32-channel chunks (else 1), 1 one tap per phase with the next chunk's halo stored
+ *   one piece per tap, 0 the same stored in one go. */
 int snrse_set_option(const char* name, int value);
 
 /* Read back a switch (any name above) or: "halo_kernel" = generation of the halo conv kernel the current

@@ -150,39 +150,50 @@ def pc_vs_golden(dev, net=None, dtype=torch.bfloat16):
     return r
 
 
-# C2-size agreement of the benched bf16 output with the fp32x3 parity mode on the same 32 clips and the same
-# Philox draws (N = 30, 60 NFE).  Measured (profiles/r04d_agree_diag.json): per-clip SI-SDR of bf16 against x3
-# 24-36 dB with a median of 32 dB, except where a clip's trajectory amplifies the bf16 rounding -- one clip of the
-# bench batch at 11 dB (rel RMS 0.27); the same clip under other Philox draws (the batch rolled by 5) agrees at 35 dB
-# and no position is systematically off, so it is a property of that (clip, noise) trajectory through 60 NFEs of a
-# formula-weight network, not of a batch slot (with the v10 kernel on the concatenated-input convs -- another fp32
-# summation order -- the same clip measured 10.5 dB, profiles/r04j_bench_line.json).  Bounds: median >= 28 dB, >= 90 %
-# of the clips >= 25 dB, mean relative RMS <= 5e-2, and every clip >= 5 dB (no trajectory diverges outright).
-C2_AGREE = {"si_sdr_median_min_db": 28.0, "frac_ge_25db_min": 0.9, "si_sdr_min_db": 5.0, "rel_rms_mean_max": 5e-2}
+# C2-size agreement of the benched bf16 output with the fp32x3 parity mode and the exact fp32 mode on the same 32 clips
+# and Philox draws (N = 30, 60 NFE; round 5, profiles/r05f_agree3.json, tools/agree3.py).  Measured: fp32x3 against
+# exact fp32 78-91 dB per clip (state distance <= 1.3e-4 relative over all 60 NFEs); bf16 against exact fp32 26-38 dB
+# (median 32) except ONE clip at 11.9 dB -- and bf16 against fp32x3 gives the same numbers to 0.01 dB, so the outlier is
+# on the bf16 side: that (clip, noise) trajectory leaves the fp32 one from NFE 3 (> 1 % state distance) and settles at
+# 21 % by NFE 50, where the other clips settle at 1.5-5 %; x3 follows fp32 on it at 82 dB.  It is a chaotic amplification
+# of bf16 rounding along one trajectory of a formula-weight network (rolled to another batch position, i.e. under other
+# draws, the same clip agrees at 35 dB: profiles/r04d_agree_diag.json), not a defect of a kernel.  Bounds: median >= 28 dB,
+# at most one clip below 25 dB, every clip >= 10 dB, mean relative RMS <= 5e-2; fp32x3 vs exact fp32: every clip >= 60 dB
+# and relative RMS <= 1e-3.
+C2_AGREE = {"si_sdr_median_min_db": 28.0, "max_clips_below_25db": 1, "si_sdr_min_db": 10.0, "rel_rms_mean_max": 5e-2}
+C2_X3_VS_FP32 = {"si_sdr_min_db": 60.0, "rel_rms_max_max": 1e-3}
 
 
-def waveform_agreement(est, ref, per_clip=False):
+def waveform_agreement(est, ref, per_clip=False, bounds=None):
     """Per-utterance agreement of waveforms est [B, L] with ref [B, L] (float64): SI-SDR of est against ref as
     the reference computes it (sgmse/util/other.py:71-75: alpha = <est, ref> / |ref|^2, 10 log10 |alpha ref|^2 /
-    |alpha ref - est|^2) and the relative RMS |est - ref| / |ref|; minimum / maximum over the batch."""
+    |alpha ref - est|^2) and the relative RMS |est - ref| / |ref|; minimum / maximum over the batch.  `bounds`: C2_AGREE
+    (default: the bf16 headline against a within-tolerance mode) or C2_X3_VS_FP32."""
+    bounds = C2_AGREE if bounds is None else bounds
     e = torch.as_tensor(est).detach().to(torch.float64)
     r = torch.as_tensor(ref).detach().to(torch.float64)
     alpha = (e * r).sum(1) / r.pow(2).sum(1)
     tgt = alpha[:, None] * r
     sisdr = 10 * torch.log10(tgt.pow(2).sum(1) / (tgt - e).pow(2).sum(1))
     relr = (e - r).pow(2).sum(1).sqrt() / r.pow(2).sum(1).sqrt()
-    out = {"si_sdr_bf16_vs_x3_db_min": float(sisdr.min()), "si_sdr_bf16_vs_x3_db_mean": float(sisdr.mean()),
-           "rel_rms_max": float(relr.max()), "rel_rms_mean": float(relr.mean()), "clips": int(e.shape[0])}
-    out["si_sdr_bf16_vs_x3_db_median"] = float(sisdr.median())
-    out["frac_clips_ge_25db"] = float((sisdr >= 25.0).double().mean())
-    out["ok"] = bool(np.isfinite(out["si_sdr_bf16_vs_x3_db_min"]) and out["si_sdr_bf16_vs_x3_db_min"] >= C2_AGREE["si_sdr_min_db"]
-                     and out["si_sdr_bf16_vs_x3_db_median"] >= C2_AGREE["si_sdr_median_min_db"]
-                     and out["frac_clips_ge_25db"] >= C2_AGREE["frac_ge_25db_min"]
-                     and out["rel_rms_mean"] <= C2_AGREE["rel_rms_mean_max"])
-    out["bounds"] = dict(C2_AGREE)
+    out = {"si_sdr_db_min": float(sisdr.min()), "si_sdr_db_mean": float(sisdr.mean()),
+           "si_sdr_db_median": float(sisdr.median()), "rel_rms_max": float(relr.max()),
+           "rel_rms_mean": float(relr.mean()), "clips": int(e.shape[0]),
+           "clips_below_25db": int((~(sisdr >= 25.0)).sum())}
+    ok = bool(np.isfinite(out["si_sdr_db_min"]) and out["si_sdr_db_min"] >= bounds["si_sdr_min_db"])
+    if "si_sdr_median_min_db" in bounds:
+        ok = ok and out["si_sdr_db_median"] >= bounds["si_sdr_median_min_db"]
+    if "max_clips_below_25db" in bounds:
+        ok = ok and out["clips_below_25db"] <= bounds["max_clips_below_25db"]
+    if "rel_rms_mean_max" in bounds:
+        ok = ok and out["rel_rms_mean"] <= bounds["rel_rms_mean_max"]
+    if "rel_rms_max_max" in bounds:
+        ok = ok and out["rel_rms_max"] <= bounds["rel_rms_max_max"]
+    out["ok"] = ok
+    out["bounds"] = dict(bounds)
     if per_clip:
         out["per_clip"] = {"si_sdr_db": [round(float(v), 2) for v in sisdr],
-                           "rel_rms": [round(float(v), 4) for v in relr],
+                           "rel_rms": [round(float(v), 6) for v in relr],
                            "ref_rms": [float(v) for v in r.pow(2).mean(1).sqrt()]}
     return out
 

@@ -103,7 +103,8 @@ struct snrse_ctx {
   int x3_tile = 0;             // split-bf16 fp32 GEMM tile: 0 auto, 1 128x128, 2 256x128, 3 128x256, 4 halo
   int x3_tw = 0;               // fp32x3 halo GEMM tile: 0 auto (8 x 32 where H % 8 == 0, W % 32 == 0), 64 = 4 x 64
   int x3_nt = 1;               // fp32x3 halo GEMM: non-temporal output stores by the epi_nt rule (+0.3 %, r04r)
-  int x3_spread = 1;           // halo split GEMM: next chunk's halo stored one piece per tap (0: in one go)
+  int x3_spread = 2;           // halo split GEMM: 2 the pair schedule (2 taps per phase), 1 one tap per phase with the next
+                               // chunk's halo stored one piece per tap, 0 the same stored in one go
   int ic_lds = 3;              // bf16 input conv: 1 the workgroup's input rows staged in LDS (W <= 1024), 2 the same
                                // with the channels split over wave pairs (4 waves / SIMD), 3 the output staged
                                // through LDS for 1-KB contiguous stores, 0 streaming loads

@@ -24,7 +24,7 @@ constexpr int KH_LDS = KH_HALO + 9 * 1024;     // + 9 taps x 16 co x 64 B = 3456
 
 SNRSE_DEV int kh_swz(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >> 1) & 3)) << 4); }
 
-#define KH_LOAD(C_, hv, wv, gs0, gs1, gh0, gh1)                                                                \
+#define KH_LOAD(C_)                                                                                            \
   do {                                                                                                         \
     const int ch_ = (C_) * 32;                                                                                 \
     const bool u1_ = ch_ >= p.C0;                                                                              \
@@ -55,7 +55,7 @@ SNRSE_DEV int kh_swz(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >
 
 // grid: B * (H / 4) * (W / 64) workgroups of 256.  GNM: 0 no prologue, 1 GroupNorm affine, 2 + SiLU
 #ifndef SNRSE_HEAD_MINB
-#define SNRSE_HEAD_MINB 2  // waves per SIMD the register allocation is bounded for (A/B builds: 3 spills)
+#define SNRSE_HEAD_MINB 1  // workgroups per CU the register allocation is bounded for (A/B builds)
 #endif
 template <int GNM>
 __global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvParams p) {
@@ -88,20 +88,16 @@ __global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvPar
     hok[j] = hr < KH_HROWS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
     hpix[j] = (b * p.H + ih) * p.W + iw;
   }
-  // two register sets (A, B): chunk c + 1's halo is loaded BEFORE chunk c's GroupNorm+SiLU transform, so a
-  // workgroup keeps one chunk's loads in flight through the whole chunk (round 4 issued them after the transform and
-  // its barrier: in flight only under the 36 short MFMAs, 2.6 TB/s at level 0 -- latency-bound)
-  u32x4 hvA[KH_HJ], wvA[KH_WJ], hvB[KH_HJ], wvB[KH_WJ];
-  f32x4 gs0A = {1.f, 1.f, 1.f, 1.f}, gs1A = gs0A, gh0A = {0.f, 0.f, 0.f, 0.f}, gh1A = gh0A;
-  f32x4 gs0B = gs0A, gs1B = gs0A, gh0B = gh0A, gh1B = gh0A;
+  u32x4 hv[KH_HJ], wv[KH_WJ];
+  f32x4 gs0 = {1.f, 1.f, 1.f, 1.f}, gs1 = gs0, gh0 = {0.f, 0.f, 0.f, 0.f}, gh1 = gh0;
 
   // acc[i]: D[co = 4 lg + e][px = w0 + 16 i + lrow]  (A = weights, B = halo pixels)
   f32x4 acc[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // registers -> LDS: GroupNorm + SiLU on the halo (rows outside the image stay zero), weights; then the 9 taps
-  auto chunk = [&](const u32x4 (&hv)[KH_HJ], const u32x4 (&wv)[KH_WJ], const f32x4& gs0, const f32x4& gs1,
-                   const f32x4& gh0, const f32x4& gh1) {
+  KH_LOAD(0);
+  for (int c = 0; c < nc; ++c) {
+    // registers -> LDS: GroupNorm + SiLU on the halo (rows outside the image stay zero), weights
 #pragma unroll
     for (int j = 0; j < KH_HJ; ++j) {
       const int hr = (tid >> 2) + 64 * j;
@@ -120,6 +116,7 @@ __global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvPar
       if (pc < KH_WP) *(u32x4*)(wsl + (pc >> 6) * 1024 + kh_swz((pc >> 2) & 15, pc & 3)) = wv[k];
     }
     __syncthreads();
+    if (c + 1 < nc) KH_LOAD(c + 1);
 #pragma unroll
     for (int tp = 0; tp < 9; ++tp) {
       const int dy = tp / 3 - 1, dx = tp % 3 - 1;
@@ -132,15 +129,6 @@ __global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvPar
       }
     }
     __syncthreads();
-  };
-  KH_LOAD(0, hvA, wvA, gs0A, gs1A, gh0A, gh1A);
-  for (int c = 0; c < nc; c += 2) {
-    if (c + 1 < nc) KH_LOAD(c + 1, hvB, wvB, gs0B, gs1B, gh0B, gh1B);
-    chunk(hvA, wvA, gs0A, gs1A, gh0A, gh1A);
-    if (c + 1 < nc) {
-      if (c + 2 < nc) KH_LOAD(c + 2, hvA, wvA, gs0A, gs1A, gh0A, gh1A);
-      chunk(hvB, wvB, gs0B, gs1B, gh0B, gh1B);
-    }
   }
   // epilogue: lanes with 4 lg < Cout hold channels 4 lg .. 4 lg + 3 of one pixel
   const int co = 4 * lg;

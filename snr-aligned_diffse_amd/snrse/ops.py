@@ -273,7 +273,9 @@ def head_ok(x, split=False):
     the fp32x3 mode's conv_head_x3_kernel)."""
     B, H, W, C = x.shape
     dt_ok = x.dtype == torch.bfloat16 or (split and x.dtype == torch.float32)
-    return dt_ok and H % 8 == 0 and W % 32 == 0 and C % 32 == 0 and _opt(x, "conv_variant") != 1
+    # channels: the C-ABI's K-tile (64 bf16 / 32 f32 channels, snrse_conv2d)
+    return dt_ok and H % 8 == 0 and W % 32 == 0 and C % (64 if x.dtype == torch.bfloat16 else 32) == 0 and \
+        _opt(x, "conv_variant") != 1
 
 
 def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):

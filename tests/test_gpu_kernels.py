@@ -618,11 +618,10 @@ def test_conv_splitk_small_levels(gpu, case):
 
 
 @pytest.mark.parametrize("shape", [(2, 128, 8, 64), (1, 256, 8, 128), (2, 128, 16, 32), (1, 256, 24, 96),
-                                   (2, 96, 16, 64), (1, 32, 8, 32)])
+                                   (2, 192, 16, 64), (1, 64, 8, 32)])
 def test_conv_head_fused_groupnorm(gpu, shape):
     """Pyramid-head conv (C -> 4, f32 out, + upsampled pyramid) consuming SiLU(GN(h)) through the
-    halo-staged head kernel (ncsnpp.py:348-366); odd and single chunk counts (C = 96, 32) exercise the two
-    alternating register sets of its halo prefetch."""
+    halo-staged head kernel (ncsnpp.py:348-366), 2 .. 8 channel chunks."""
     from snrse import ops
     B, C, H, W = shape
     x = (torch.from_numpy(fnormal("t.hd.x", (B, C, H, W))) * 1.5 + 0.2).bfloat16().float()

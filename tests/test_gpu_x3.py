@@ -224,14 +224,14 @@ def test_x3h_fused_groupnorm_silu(gpu, shape, act, spread):
     with pytest.raises(RuntimeError):
         ops.conv2d(s0, wp, 3, cout, src1=s1, gn=gn, gn_act=act, sc=nhwc(xs).to(gpu), sc_wgt=w2p)
     ops.set_option("x3_tile", 4)
-    ops.set_option("x3_spread", spread)  # next chunk's halo stored one piece per tap (1) or in one go (0)
+    ops.set_option("x3_spread", spread)  # pair schedule (2), halo stored one piece per tap (1) or in one go (0)
     try:
         assert ops.x3h_ok(s0, 3, cout)
         out = ops.conv2d(s0, wp, 3, cout, src1=s1, gn=gn, gn_act=act, sc=nhwc(xs).to(gpu), sc_wgt=w2p)
         assert ops.get_option("last_kernel") == 4
     finally:
         ops.set_option("x3_tile", 0)
-        ops.set_option("x3_spread", 1)
+        ops.set_option("x3_spread", 2)
     assert rel(nchw(out), ref) < TOL
 
 

@@ -1,6 +1,7 @@
 """CPU tests of the host-side agreement logic bench.py writes into its line (paritycheck.waveform_agreement:
 parity_mode.c2_agreement, bounded by paritycheck.C2_AGREE): per-clip SI-SDR as the reference computes it
-(sgmse/util/other.py:71-75) and the distribution bounds (median, fraction >= 25 dB, floor, mean relative RMS)."""
+(sgmse/util/other.py:71-75) and the distribution bounds (median, clips below 25 dB, floor, mean relative RMS; the
+fp32x3-vs-exact-fp32 bounds)."""
 import math
 
 import numpy as np
@@ -26,23 +27,39 @@ def test_si_sdr_matches_the_reference_formula():
         alpha = float((e * x).sum() / (x * x).sum())
         want = 10 * math.log10(float((alpha * x).pow(2).sum() / (alpha * x - e).pow(2).sum()))
         assert abs(r["per_clip"]["si_sdr_db"][k] - want) < 0.01
-    assert abs(r["si_sdr_bf16_vs_x3_db_median"] - 20.0) < 0.5
+    assert abs(r["si_sdr_db_median"] - 20.0) < 0.5
 
 
 def test_bounds_accept_one_outlier_and_reject_a_shifted_distribution():
     snr = np.full(32, 32.0)
-    snr[0] = 11.0  # the measured outlier (profiles/r04d_agree_diag.json)
+    snr[0] = 11.9  # the measured outlier, bf16 against exact fp32 (profiles/r05f_agree3.json)
     est, ref = _pair(32, snr)
     ok = paritycheck.waveform_agreement(est, ref)
-    assert ok["ok"] and ok["frac_clips_ge_25db"] > 0.95 and ok["si_sdr_bf16_vs_x3_db_min"] < 12
-    # every clip 24 dB: median and fraction bounds fail
+    assert ok["ok"] and ok["clips_below_25db"] == 1 and ok["si_sdr_db_min"] < 12.5
+    # every clip 24 dB: median and clip-count bounds fail
     est, ref = _pair(32, np.full(32, 24.0))
     assert not paritycheck.waveform_agreement(est, ref)["ok"]
-    # one clip diverged outright (below the 5 dB floor)
-    snr[3] = 2.0
-    est, ref = _pair(32, snr)
+    # a second clip below 25 dB (a regression that hits more than the one known trajectory)
+    snr2 = snr.copy()
+    snr2[5] = 20.0
+    est, ref = _pair(32, snr2)
+    assert not paritycheck.waveform_agreement(est, ref)["ok"]
+    # the outlier itself falling below the 10 dB floor
+    snr3 = snr.copy()
+    snr3[0] = 8.0
+    est, ref = _pair(32, snr3)
     assert not paritycheck.waveform_agreement(est, ref)["ok"]
     # NaN output anywhere
     est, ref = _pair(32, np.full(32, 32.0))
     est[5, 7] = float("nan")
     assert not paritycheck.waveform_agreement(est, ref)["ok"]
+
+
+def test_x3_vs_fp32_bounds():
+    b = paritycheck.C2_X3_VS_FP32
+    est, ref = _pair(32, np.full(32, 78.0))  # the measured floor of fp32x3 against exact fp32
+    assert paritycheck.waveform_agreement(est, ref, bounds=b)["ok"]
+    snr = np.full(32, 85.0)
+    snr[3] = 50.0
+    est, ref = _pair(32, snr)
+    assert not paritycheck.waveform_agreement(est, ref, bounds=b)["ok"]

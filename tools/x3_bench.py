@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--tiles", default="0,1,3")
     ap.add_argument("--exact", type=int, default=1)
     ap.add_argument("--gn", type=int, default=0, help="1: fused GroupNorm+SiLU on the x3h variants (x3_tile 0)")
-    ap.add_argument("--spread", default="1", help="x3_spread settings to run each split variant with")
+    ap.add_argument("--spread", default="2", help="x3_spread settings to run each split variant with")
     ap.add_argument("--shapes", default="", help="comma list of SHAPES indices (default all)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -79,7 +79,7 @@ def main():
                               "tflops": flops / ms / 1e9, "kernel": ops.kernel_name(ops.get_option("last_kernel")),
                               "ksplit": ops.get_option("last_ksplit"), "rel_vs_first": err}), flush=True)
         ops.set_option("x3_tile", 0)
-        ops.set_option("x3_spread", 1)
+        ops.set_option("x3_spread", 2)
         del x0, x1, out, ref
 
 
