@@ -566,8 +566,8 @@ def run(args):
         by = probe.summary()
         per_kernel = {k: {"launches": v[2], "ms": v[1], "tflops": v[0] / max(v[1], 1e-9) / 1e9,
                           "frac": v[0] / max(v[1], 1e-9) * 1e3 / PEAK[args.dtype]} for k, v in by.items()}
-        # the ResBlock 3x3 halo GEMMs run as two kernels split by shape (option h10 = 2: v10 takes the concatenated-
-        # input convs, v5 the rest): reported as one family, the sum of their FLOPs over the sum of their launch times
+        # (rounds 4-5 ran the ResBlock 3x3 convs on two kernels split by shape, reported as one family -- the sum of
+        # their FLOPs over the sum of their launch times; since round 5 one kernel, conv_halo5_kernel, runs them all)
         fam = [k for k in ("conv_halo5_kernel", "conv_halo10_kernel") if k in by]
         if len(fam) == 2:
             by["+".join(fam)] = [sum(by[k][i] for k in fam) for i in range(3)]

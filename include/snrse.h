@@ -161,9 +161,6 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  *   2 256 x 128, 3 128 x 256 (Cout % 256 == 0), 4 the halo kernel wherever its shape conditions hold;
  * "stats_zeroed" 1 = the statistics buffers handed to snrse_conv2d / snrse_gn_stats are already zero (the
  * caller clears one arena per network evaluation), so they skip their per-call memset;
- * "h10" the v10 halo GEMM under conv_variant 0 (conv_variant 10 forces it): 2 (default) the concatenated-input
- *   3x3 convs without a shortcut, 3 those and the convs whose fused 1x1 shortcut spans twice their input
- *   channels, 1 every conv the v5 halo GEMM would take, 0 off;
  * "ic_lds" the bf16 input conv (W <= 1024): 3 (default) its workgroup's input rows staged in LDS and its output
  *   staged through LDS for whole-KB stores, 1 input rows only, 2 with the channels split over wave pairs, 0 the
  *   streaming form (all bit-identical but 2's statistics fold order);
@@ -175,11 +172,11 @@ int snrse_set_workspace(void* ptr, size_t bytes);
 int snrse_set_option(const char* name, int value);
 
 /* Read back a switch (any name above) or: "halo_kernel" = generation of the halo conv kernel the current
- * setting dispatches a single-input conv to (5, or 12 under h10 = 1), "last_kernel" = generation of the most recent snrse_conv2d launch (1 v1, 2 v2,
- * 3 / 4 split-bf16 register-staged / halo, 5 halo, 10 pyramid head, 11 split-bf16 pyramid head, 12 v10 halo),
+ * setting dispatches a 3x3 conv to (5), "last_kernel" = generation of the most recent snrse_conv2d launch (1 v1, 2 v2,
+ * 3 / 4 split-bf16 register-staged / halo, 5 halo, 10 pyramid head, 11 split-bf16 pyramid head),
  * "last_ksplit" = K splits of the most recent v2 launch, "last_epi_nt" /
  * "last_chunks" = store flavour / image-range launches of the most recent halo conv, "last_tw" = its tile
- * width (32 / 64; 32 for the v10 halo GEMM, whose tiles are 16 x 32 px). */
+ * width (32 / 64). */
 int snrse_get_option(const char* name, int* value);
 
 /* AttnBlockpp attention core (layerspp.py:84-88): qkv [B][L][3C] -> out [B][L][C],

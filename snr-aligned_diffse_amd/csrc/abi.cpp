@@ -57,7 +57,6 @@ int* option_field(snrse_ctx& c, const char* name) {
   if (name_is(name, "resample_down_rows")) return &c.resample_down_rows;
   if (name_is(name, "x3_tile")) return &c.x3_tile;
   if (name_is(name, "x3_spread")) return &c.x3_spread;
-  if (name_is(name, "h10")) return &c.h10;
   if (name_is(name, "ic_lds")) return &c.ic_lds;
   if (name_is(name, "x3_nt")) return &c.x3_nt;
   if (name_is(name, "x3_tw")) return &c.x3_tw;
@@ -77,8 +76,7 @@ int set_option(snrse_ctx& c, const char* name, int value) {
 int get_option(const snrse_ctx& c, const char* name, int* value) {
   if (!name || !value) return SNRSE_EINVAL;
   if (const int* f = option_field(const_cast<snrse_ctx&>(c), name)) { *value = *f; return 0; }
-  if (name_is(name, "halo_kernel")) { *value = c.h10 == 1 ? 12 : 5; return 0; }  // the halo generation variant 0 takes
-  // for a single-input conv (under h10 = 2 the concatenated-input ones without a shortcut take 12)
+  if (name_is(name, "halo_kernel")) { *value = 5; return 0; }  // the halo generation variant 0 takes
   if (name_is(name, "last_kernel")) { *value = c.last_kernel; return 0; }
   if (name_is(name, "last_ksplit")) { *value = c.last_ksplit; return 0; }
   if (name_is(name, "last_epi_nt")) { *value = c.last_epi_nt; return 0; }

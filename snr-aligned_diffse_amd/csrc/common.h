@@ -108,10 +108,6 @@ struct snrse_ctx {
   int ic_lds = 3;              // bf16 input conv: 1 the workgroup's input rows staged in LDS (W <= 1024), 2 the same
                                // with the channels split over wave pairs (4 waves / SIMD), 3 the output staged
                                // through LDS for 1-KB contiguous stores, 0 streaming loads
-  int h10 = 2;                 // v10 halo GEMM under conv_variant 0: 1 = every bf16 3x3 conv v5 takes,
-                               // 2 = the concatenated-input ones without a shortcut, 3 = those and the
-                               // ones with a shortcut of twice their input channels, 0 = off
-  int num_cu = 0;              // compute units of the device (v10 persistent grid), read on first use
   // split-K workspace: [splits][M][Cout] f32 partial sums (NULL: no splitting)
   float* ws = nullptr;
   size_t ws_bytes = 0;

@@ -1035,8 +1035,8 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
     // (chunk c0 + s / 9, tap s % 9) from ring slot `so`; at its top it waits for its own DMA (issued at the top of
     // phase k - 1; the halo prefetch issued behind that DMA at phase 0 / 4 may stay in flight), then issues the next
     // phase's DMA.  The halo of chunk c + 1 is prefetched at the phase holding tap (c, 0) and stored, split (+
-    // GroupNorm), one piece after each of the taps (c, 2 .. 7) into the other halo buffer (HJ = 6 pieces at TW 32);
-    // the last piece lands a barrier before tap (c + 1, 0) is read.  Then the shortcut chunks, one tap per phase.
+    // GroupNorm), after the taps (c, 4 .. 7) into the other halo buffer (HJ = 6 pieces at TW 32); the last piece lands
+    // a barrier before tap (c + 1, 0) is read.  Then the shortcut chunks, one tap per phase.
     static_assert(TW == 32 && HJ == 6, "pair schedule: 8 x 32 tiles, 6 halo pieces per thread");
     constexpr int SLOT2 = 2 * TAPB;
     int so = 0;
@@ -1080,14 +1080,20 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
           }
         }
         const char* const sl_ = ring + so;
-        // tap A, then its halo piece; tap B, then its piece.  Piece j of chunk c's successor after tap (c, 2 + j);
-        // before the first one (tap 2) the halo loads are waited for (only this phase's 4 DMA pieces are younger)
+        // tap A, then its halo pieces; tap B, then its pieces.  The 6 pieces of chunk c's successor go after taps
+        // (c, 4) [0, 1], (c, 5) [2, 3], (c, 6) [4], (c, 7) [5]: taps 4.. lie in the phases whose top wait already
+        // drained the prefetch (phases 2 and 6), so the loads have 4 taps of cover and no piece waits on them (pieces
+        // after taps 2 and 3 waited for HBM inside phases 1 / 5: ~12 % of the launch, profiles/r05g_x3h_ablations)
         auto piece_after = [&](int d, int t) {
           const int c = c0 + d;
-          if (t < 2 || t > 7) return;
+          if (t < 4 || t > 7) return;
           if (d == 1 && !pf1) return;
-          if (t == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-          halo_piece(smem + ((c + 1) & 1) * HBYTES, t - 2, c + 1 < cbm);
+          char* const nb_ = smem + ((c + 1) & 1) * HBYTES;
+          const bool tr = c + 1 < cbm;
+          if (t == 4) { halo_piece(nb_, 0, tr); halo_piece(nb_, 1, tr); }
+          if (t == 5) { halo_piece(nb_, 2, tr); halo_piece(nb_, 3, tr); }
+          if (t == 6) halo_piece(nb_, 4, tr);
+          if (t == 7) halo_piece(nb_, 5, tr);
         };
         tap_mfma(smem + ((c0 + da) & 1) * HBYTES, sl_, ta);
         piece_after(da, ta);
@@ -2089,31 +2095,9 @@ int dispatch_conv(const ConvParams& p, hipStream_t s, snrse_ctx& cx) {
       if (cx.conv_variant != 1 && fits) {
         // halo path on the 4 x 64-tileable images (levels 0-3 of the C2 pyramid), with 8 x 32 tiles where
         // H % 8 == 0.  Not on W = 32 (level 4): 128 tiles for 512 workgroup slots ran 11-45 % slower there
-        // than the split-K LDS-DMA GEMM + gn_act (profiles/r03v_level4_halo_vs_glds.jsonl)
-        if constexpr (sizeof(TO) == 2) {
-          // v10 (conv_h10.hip): forced by conv_variant 10; taken by variant 0 on v5's shapes under option h10 = 1, and under
-          // h10 = 2 for the concatenated-input convs without a shortcut (the up path's Conv_0, where it measured ~4 %
-          // faster than v5: 8 chunks per tile amortise its epilogue; profiles/r04_v10_ablations.jsonl)
-          // h10 = 3 adds the convs whose fused shortcut spans twice their input (the up path's Conv_1 over cat(h, skip))
-          const bool h10_cat = p.C1 > 0 && !p.sc_src;
-          const bool h10_sc2 = p.sc_src && p.Csc + p.Csc1 == 2 * (p.C0 + p.C1);
-          const bool h10_auto = cx.conv_variant == 0 && halo_tile64(p) &&
-                                (cx.h10 == 1 || (cx.h10 == 2 && h10_cat) || (cx.h10 == 3 && (h10_cat || h10_sc2)));
-          if ((cx.conv_variant == 10 || h10_auto) && h10_ok(p)) {
-            if (!cx.num_cu) {
-              int dev = 0;
-              SNRSE_RET(hipGetDevice(&dev));
-              SNRSE_RET(hipDeviceGetAttribute(&cx.num_cu, hipDeviceAttributeMultiprocessorCount, dev));
-            }
-            cx.last_kernel = 12;
-            cx.last_tw = kH10TileW;
-            cx.last_ksplit = 1;
-            ConvParams q = p;  // (non-temporal output stores as the v5 launch decides them)
-            q.epi_nt = cx.epi_nt == 2 ? ((long long)p.M * p.out_ld * 2ll > ((long long)cx.epi_nt_mb << 20)) : cx.epi_nt;
-            cx.last_epi_nt = q.epi_nt;
-            return launch_h10(q, s, cx.num_cu, cx.h5_specialise != 0);
-          }
-        }
+        // than the split-K LDS-DMA GEMM + gn_act (profiles/r03v_level4_halo_vs_glds.jsonl).  (Round 4's v10 halo GEMM,
+        // one wave per SIMD with 512 registers, ran the concatenated-input Conv_0s until round 5's v5 changes made v5
+        // 4 % faster there and +0.4 % on the C2 line, profiles/r05h_*; it was removed -- git history, conv_h10.hip.)
         if (cx.conv_variant != 2 && p.ksize == 3 && halo_tile64(p)) {
           cx.last_kernel = kHaloAuto;
           return launch_halo5<TO>(p, s, cx);

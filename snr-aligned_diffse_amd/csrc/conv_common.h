@@ -105,10 +105,6 @@ SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
 
 // Pyramid heads (conv_head.hip): 3x3, Cout <= 16, f32 output, optional fused GroupNorm+SiLU.
 int launch_head(const ConvParams& p, hipStream_t s);
-// v10 halo GEMM (conv_h10.hip): persistent, one wave per SIMD, 16 x 32 px x 128 cout tiles, fused 1x1 shortcut
-bool h10_ok(const ConvParams& p);
-constexpr int kH10TileW = 32;  // its tile width (snrse_get_option "last_tw")
-int launch_h10(ConvParams p, hipStream_t s, int num_cu, bool specialise);
 int launch_head_x3(const ConvParams& p, hipStream_t s);
 bool head_ok(const ConvParams& p);
 
