@@ -168,12 +168,15 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  *   4 x 64; "x3_nt" 1 (default) its fp32 output stores non-temporal under the "epi_nt" rule;
  * "x3_spread" fp32x3 halo GEMM schedule: 2 (default) two taps per barrier phase where its tiles are 8 x 32 px and the
  *   main input has an even number of 32-channel chunks (else 1), 1 one tap per phase with the next chunk's halo stored
- *   one piece per tap, 0 the same stored in one go. */
+ *   one piece per tap, 0 the same stored in one go;
+ * "head_small" bf16 pyramid heads (Cout 4, C % 256 == 0): 1 (default) the wave-per-8-pixels head (GroupNorm fused)
+ *   where the tiled head cannot take the image (H % 8 or W % 32 != 0), 2 also for up to 16384 output pixels, 0 never. */
 int snrse_set_option(const char* name, int value);
 
 /* Read back a switch (any name above) or: "halo_kernel" = generation of the halo conv kernel the current
  * setting dispatches a 3x3 conv to (5), "last_kernel" = generation of the most recent snrse_conv2d launch (1 v1, 2 v2,
- * 3 / 4 split-bf16 register-staged / halo, 5 halo, 10 pyramid head, 11 split-bf16 pyramid head),
+ * 3 / 4 split-bf16 register-staged / halo, 5 halo, 10 pyramid head, 11 split-bf16 pyramid head, 14 small-image
+ * pyramid head),
  * "last_ksplit" = K splits of the most recent v2 launch, "last_epi_nt" /
  * "last_chunks" = store flavour / image-range launches of the most recent halo conv, "last_tw" = its tile
  * width (32 / 64). */
@@ -186,6 +189,11 @@ int snrse_attention(const void* qkv, void* out, int B, int L, int C, int dtype, 
 /* Time embedding (ncsnpp.py:256-275): temb[b] = W2 silu(W1 [sin, cos](2 pi log t W_gfp) + b1) + b2. */
 int snrse_temb_mlp(const float* t, const float* Wg, const float* W1, const float* b1, const float* W2,
                    const float* b2, float* temb, int B, int nf, hipStream_t stream);
+/* The same MLP as two row-parallel launches (the form the network executor runs; every weight row is read once
+ * per launch, spread over the chip): snrse_temb_gfp_dense gives the pre-activation a[b] = W1 [sin, cos](2 pi log t
+ * W_gfp) + b1 (out [B][4 nf]), then snrse_temb_dense(a, W2, b2) = W2 silu(a) + b2 = temb.  nf even, 2 nf <= 512. */
+int snrse_temb_gfp_dense(const float* t, const float* Wg, const float* W1, const float* b1, float* out, int B, int nf,
+                         hipStream_t stream);
 /* All ResBlock Dense_0 projections (layerspp.py:264-265): out[b][r] = W[r] . silu(temb[b]) + bias[r]. */
 int snrse_temb_dense(const float* temb, const float* W, const float* bias, float* out, int B, int R, int D,
                      hipStream_t stream);

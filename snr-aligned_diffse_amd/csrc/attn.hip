@@ -78,9 +78,50 @@ __global__ __launch_bounds__(64 * AttnCfg<T>::NW) void attn_kernel(const T* qkv,
   for (int e = 0; e < 4; ++e) { m_run[e] = -INFINITY; l_run[e] = 0.f; }
 
   char* Pw = Ps + wid * P_BYTES;
+  // bf16: the next K / V block is loaded into registers while the current one is consumed, and V is
+  // transposed in registers (8 keys x 8 channels per thread, v_perm) so it lands in LDS as 16-B stores
+  // (the per-element 2-B stores of the generic path held the level-4 attention at ~67 us;
+  // profiles/r05a_c2_dispatch_shapes.jsonl)
+  constexpr bool kPipe = sizeof(T) == 2 && KB * CPR == 8 * NTH && (KB / 8) * CPR == NTH;
+  u32x4 kreg[kPipe ? 8 : 1], vreg[kPipe ? 8 : 1];
+  auto load_kv = [&](int kb0) {
+    if constexpr (kPipe) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {  // K: 16-B chunk i = tid + NTH j
+        const int i = tid + NTH * j, r = i / CPR, cc = i % CPR;
+        kreg[j] = (kb0 + r < L) ? *(const u32x4*)(base + (size_t)(kb0 + r) * ld + C + cc * EPC) : u32x4{0u, 0u, 0u, 0u};
+      }
+      const int kg = tid / CPR, cc = tid % CPR;  // V: keys 8 kg .. 8 kg + 7 of channel chunk cc
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = 8 * kg + q;
+        vreg[q] = (kb0 + r < L) ? *(const u32x4*)(base + (size_t)(kb0 + r) * ld + 2 * C + cc * EPC) : u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+  };
+  if constexpr (kPipe) load_kv(0);
   for (int k0 = 0; k0 < L; k0 += KB) {
     __syncthreads();  // previous tile fully consumed
-    for (int i = tid; i < KB * CPR; i += NTH) {
+    if constexpr (kPipe) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = tid + NTH * j, r = i / CPR, cc = i % CPR;
+        *(u32x4*)(Ks + (cc / 8) * KB * 128 + swz(r, cc % 8)) = kreg[j];
+      }
+      const int kg = tid / CPR, cc = tid % CPR;
+      // out row c' (channel 8 cc + c'), word i = keys (2i, 2i+1): halves of word c' / 2 of key rows 2i, 2i+1
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const unsigned sel = (c & 1) ? 0x07060302u : 0x05040100u;
+        u32x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = __builtin_amdgcn_perm(vreg[2 * i + 1][c >> 1], vreg[2 * i][c >> 1], sel);
+        *(u32x4*)(Vs + swz(cc * 8 + c, kg)) = o;
+      }
+      __syncthreads();
+      if (k0 + KB < L) load_kv(k0 + KB);
+    }
+    for (int i = tid; !kPipe && i < KB * CPR; i += NTH) {
       const int r = i / CPR, cc = i % CPR;
       const int kb = cc / 8, ch = cc % 8;
       u32x4 kv = u32x4{0u, 0u, 0u, 0u}, vv = u32x4{0u, 0u, 0u, 0u};
@@ -98,7 +139,7 @@ __global__ __launch_bounds__(64 * AttnCfg<T>::NW) void attn_kernel(const T* qkv,
         *(T*)(Vs + swz(c, kch) + kin * (int)sizeof(T)) = ve[e];
       }
     }
-    __syncthreads();
+    if constexpr (!kPipe) __syncthreads();
 
     // S = Q K^T  (16 x KB per wave)
     f32x4 s[SJ];

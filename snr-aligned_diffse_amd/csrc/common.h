@@ -67,6 +67,34 @@ SNRSE_DEV float wave_max(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+// Sum of N per-lane partial vectors over the wave (N a power of two <= 64), transposed: lane l returns the
+// full sum of element l % N.  Butterfly: at the stage of lane bit b a lane keeps the half of its elements whose
+// index bit b equals its own lane bit and adds the partner's copy of them (N - 1 shuffles for N sums, instead of
+// 6 N for N separate wave reductions); the lane bits above log2 N are folded at the end.
+template <int N>
+SNRSE_DEV float bfly_sum(float (&p)[N], int lane) {
+  static_assert(N >= 1 && N <= 64 && (N & (N - 1)) == 0, "N: power of two <= 64");
+  int lb = 0;
+#pragma unroll
+  for (int n = N; n > 1; n >>= 1, ++lb) {
+    const bool hi = (lane >> lb) & 1;
+#pragma unroll
+    for (int i = 0; i < n / 2; ++i) {
+      const float keep = hi ? p[2 * i + 1] : p[2 * i];
+      const float send = hi ? p[2 * i] : p[2 * i + 1];
+      p[i] = keep + __shfl_xor(send, 1 << lb, 64);
+    }
+  }
+  float v = p[0];
+#pragma unroll
+  for (int b = lb; b < 6; ++b) v += __shfl_xor(v, 1 << b, 64);
+  return v;
+}
+
+SNRSE_DEV float dot4(const f32x4& a, const f32x4& b) {
+  return fmaf(a[0], b[0], fmaf(a[1], b[1], fmaf(a[2], b[2], a[3] * b[3])));
+}
+
 SNRSE_DEV double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -105,6 +133,8 @@ struct snrse_ctx {
   int x3_nt = 1;               // fp32x3 halo GEMM: non-temporal output stores by the epi_nt rule (+0.3 %, r04r)
   int x3_spread = 2;           // halo split GEMM: 2 the pair schedule (2 taps per phase), 1 one tap per phase with the next
                                // chunk's halo stored one piece per tap, 0 the same stored in one go
+  int head_small = 1;          // pyramid heads (Cout 4, bf16): 1 the wave-per-8-pixels kernel where the tiled head cannot
+                               // take the image (H % 8 or W % 32), 2 also for <= 16384 output pixels, 0 never
   int ic_lds = 3;              // bf16 input conv: 1 the workgroup's input rows staged in LDS (W <= 1024), 2 the same
                                // with the channels split over wave pairs (4 waves / SIMD), 3 the output staged
                                // through LDS for 1-KB contiguous stores, 0 streaming loads

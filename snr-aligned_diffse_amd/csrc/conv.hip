@@ -92,13 +92,47 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
   }
   const int m_last = min(mb + nvalid - 1, p.M - 1);
   const bool one_b = mb < p.M && (mb / HW) == (m_last / HW);
+  const int slot = blockIdx.x & (SNRSE_STAT_SLOTS - 1);
+  // A wave tile spanning several images (HW < 64: the 4 x 8 level of the C2 pyramid) with HW % RPP == 0:
+  // every pass's RPP rows lie in one image, so the image is wave-uniform per pass and the statistics are
+  // reduced per image run (one atomic pair per channel and image) instead of per element (per-element f64
+  // atomics made a 1024-px 1x1 conv take 156 us, profiles/r05a_c2_dispatch_shapes.jsonl).
+  const bool seg = p.stats && !one_b && HW % RPP == 0;
+  int seg_b = -1;
   float s1[EPC], s2[EPC];
 #pragma unroll
   for (int k = 0; k < EPC; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+  auto seg_flush = [&]() {
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) {
+#pragma unroll
+      for (int o = NCH; o < 64; o <<= 1) {
+        s1[k] += __shfl_xor(s1[k], o, 64);
+        s2[k] += __shfl_xor(s2[k], o, 64);
+      }
+    }
+    if (r0 == 0 && nok && seg_b >= 0 && (long long)seg_b * HW < p.M) {
+      const size_t base = stat_idx(seg_b, slot, n, p.Cout);
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) {
+        unsafeAtomicAdd(&p.stats[base + 2 * k], (double)s1[k]);
+        unsafeAtomicAdd(&p.stats[base + 2 * k + 1], (double)s2[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
+  };
 #pragma unroll
   for (int pass = 0; pass < 64 / RPP; ++pass) {
     const int row = r0 + pass * RPP;
     const int m = mb + row;
+    if (seg) {
+      const int bp = (mb + pass * RPP) / HW;  // wave-uniform
+      if (bp != seg_b) {
+        if (seg_b >= 0) seg_flush();
+        seg_b = bp;
+      }
+    }
     if (m >= p.M || !nok || row >= nvalid) continue;
     float v[EPC];
     const float* sr = stage + row * LDR + cc * EPC;
@@ -142,19 +176,20 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
     else
       *(u32x4*)((TO*)p.out + (size_t)m * p.out_ld + n) = o;
     if (p.stats) {
-      if (one_b) {
+      if (one_b || seg) {
 #pragma unroll
         for (int k = 0; k < EPC; ++k) { s1[k] += v[k]; s2[k] = fmaf(v[k], v[k], s2[k]); }
       } else {
 #pragma unroll
         for (int k = 0; k < EPC; ++k) {
-          const size_t o = stat_idx(m / HW, blockIdx.x & (SNRSE_STAT_SLOTS - 1), n + k, p.Cout);
+          const size_t o = stat_idx(m / HW, slot, n + k, p.Cout);
           unsafeAtomicAdd(&p.stats[o], (double)v[k]);
           unsafeAtomicAdd(&p.stats[o + 1], (double)v[k] * v[k]);
         }
       }
     }
   }
+  if (seg && seg_b >= 0) seg_flush();
   if (p.stats && one_b) {
 #pragma unroll
     for (int k = 0; k < EPC; ++k) {
@@ -165,7 +200,6 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
       }
     }
   }
-  const int slot = blockIdx.x & (SNRSE_STAT_SLOTS - 1);
   if (p.stats && blk_b >= 0) {  // uniform over the block
     if (r0 == 0) {
 #pragma unroll
@@ -2113,9 +2147,17 @@ int dispatch_conv(const ConvParams& p, hipStream_t s, snrse_ctx& cx) {
     return launch_conv<T, TO, 128, 128, 2, 2>(p, p.Cout, s, cx);
   }
   if constexpr (sizeof(T) == 2 && sizeof(TO) == 4) {
-    if (cx.conv_variant != 1 && head_ok(p)) {
+    // small images (option head_small 2: also where the tiled head fits, up to 16384 output pixels) take the
+    // wave-per-8-pixels head
+    const bool small = cx.head_small == 2 && (long long)p.B * p.H * p.W <= 16384;
+    if (cx.conv_variant != 1 && head_ok(p) && !small) {
       cx.last_kernel = 10;
       return launch_head(p, s);
+    }
+    if (cx.conv_variant != 1 && cx.head_small && head_small_ok(p)) {
+      cx.last_kernel = 14;
+      cx.last_ksplit = 1;
+      return launch_head_small(p, s);
     }
   }
   if (p.gn_scale) return SNRSE_EINVAL;

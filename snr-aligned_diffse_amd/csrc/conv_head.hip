@@ -297,6 +297,115 @@ __global__ __launch_bounds__(256) void conv_head_x3_kernel(ConvParams p) {
 
 }  // namespace
 
+// Pyramid heads of the levels the tiled kernel cannot take (H % 8 or W % 32 != 0: the 8 x 16 and 4 x 8 levels
+// of the C2 pyramid, ncsnpp.py:348-366).  They ran on the register-staged GEMM (conv_mfma_kernel, 8-32
+// workgroups walking 36 K-tiles: ~46 us per launch, profiles/r05a_c2_dispatch_shapes.jsonl) after a separate
+// gn_act pass.  Here one wave owns PX = 8 consecutive output pixels of one row; a lane owns 4 input channels of
+// every 256-channel pass and keeps their 9 taps x 4 output channels of weights in registers (packed bf16);
+// each of the 3 x (PX + 2) input pixels is loaded once (8 B per lane), GroupNorm(+SiLU)-transformed in fp32
+// (zero padding stays zero) and accumulated into the up to 3 output pixels it feeds.  The PX x 4 per-lane
+// partial sums are reduced across the wave with bfly_sum<32>, which leaves lane l with output (px l / 4,
+// co l % 4): the 32 results are one contiguous 128-B f32 store.  Cout == 4, C1 == 0, C0 % 256 == 0.
+constexpr int KS_PX = 8;
+
+template <int GNM>
+__global__ __launch_bounds__(256) void conv_head_small_kernel(ConvParams p) {
+  const int lane = threadIdx.x & 63;
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nxw = (p.W + KS_PX - 1) / KS_PX;
+  if (wv >= p.B * p.H * nxw) return;  // wave-uniform: whole waves past the end
+  const int xw = wv % nxw;
+  const int t = wv / nxw;
+  const int y = t % p.H, b = t / p.H;
+  const int x0 = xw * KS_PX;
+  const int C = p.C0, K1 = 9 * C;
+  const bf16_t* src = (const bf16_t*)p.src0;
+  const bf16_t* wg = (const bf16_t*)p.wgt;
+  float acc[KS_PX][4];
+#pragma unroll
+  for (int i = 0; i < KS_PX; ++i)
+#pragma unroll
+    for (int co = 0; co < 4; ++co) acc[i][co] = 0.f;
+  for (int c0 = 0; c0 < C; c0 += 256) {
+    const int c = c0 + 4 * lane;
+    uint2 wq[9][4];
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+      for (int co = 0; co < 4; ++co) wq[tp][co] = *(const uint2*)(wg + (size_t)co * K1 + tp * C + c);
+    f32x4 gs = {1.f, 1.f, 1.f, 1.f}, gh = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (GNM > 0) {
+      gs = *(const f32x4*)(p.gn_scale + (size_t)b * C + c);
+      gh = *(const f32x4*)(p.gn_shift + (size_t)b * C + c);
+    }
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int yy = y + dy;
+      if (yy < 0 || yy >= p.H) continue;  // wave-uniform
+#pragma unroll
+      for (int j = 0; j < KS_PX + 2; ++j) {
+        const int xx = x0 - 1 + j;
+        if (xx < 0 || xx >= p.W) continue;  // wave-uniform
+        const uint2 raw = *(const uint2*)(src + (((size_t)b * p.H + yy) * p.W + xx) * C + c);
+        float v[4] = {__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u),
+                      __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
+        if constexpr (GNM > 0) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float a = fmaf(v[e], gs[e], gh[e]);
+            v[e] = GNM == 2 ? silu(a) : a;
+          }
+        }
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          const int i = j - 1 - dx;  // the output pixel x0 + i reads this column through tap dx
+          if (i < 0 || i >= KS_PX) continue;
+          const int tp = (dy + 1) * 3 + dx + 1;
+#pragma unroll
+          for (int co = 0; co < 4; ++co) {
+            const uint2 w = wq[tp][co];
+            float a = acc[i][co];
+            a = fmaf(v[0], __uint_as_float(w.x << 16), a);
+            a = fmaf(v[1], __uint_as_float(w.x & 0xffff0000u), a);
+            a = fmaf(v[2], __uint_as_float(w.y << 16), a);
+            a = fmaf(v[3], __uint_as_float(w.y & 0xffff0000u), a);
+            acc[i][co] = a;
+          }
+        }
+      }
+    }
+  }
+  float pp[4 * KS_PX];
+#pragma unroll
+  for (int i = 0; i < KS_PX; ++i)
+#pragma unroll
+    for (int co = 0; co < 4; ++co) pp[4 * i + co] = acc[i][co];
+  const float s = bfly_sum<4 * KS_PX>(pp, lane);
+  const int i = (lane & 31) >> 2, co = lane & 3, x = x0 + i;
+  if (lane < 32 && x < p.W) {
+    const size_t m = ((size_t)b * p.H + y) * p.W + x;
+    float o = s + (p.bias ? p.bias[co] : 0.f);
+    if (p.res) o += ((const float*)p.res)[m * p.res_ld + co];
+    ((float*)p.out)[m * p.out_ld + co] = o * p.out_scale;
+  }
+}
+
+bool head_small_ok(const ConvParams& p) {
+  if (p.ksize != 3 || p.Cout != 4 || p.C1 != 0 || p.C0 <= 0 || p.C0 % 256 || p.B <= 0) return false;
+  if (p.sc_src || p.temb || p.comb_src || p.stats) return false;
+  return (long long)p.B * p.H * ((p.W + KS_PX - 1) / KS_PX) < 0x7fffffffLL;
+}
+
+int launch_head_small(const ConvParams& p, hipStream_t s) {
+  if (!head_small_ok(p)) return SNRSE_EINVAL;
+  const long long waves = (long long)p.B * p.H * ((p.W + KS_PX - 1) / KS_PX);
+  const unsigned blocks = (unsigned)((waves + 3) / 4);
+  if (!p.gn_scale) hipLaunchKernelGGL(conv_head_small_kernel<0>, dim3(blocks), dim3(256), 0, s, p);
+  else if (!p.gn_act) hipLaunchKernelGGL(conv_head_small_kernel<1>, dim3(blocks), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(conv_head_small_kernel<2>, dim3(blocks), dim3(256), 0, s, p);
+  return (int)hipGetLastError();
+}
+
 bool head_ok(const ConvParams& p) {
   if (p.ksize != 3 || p.Cout > 16 || p.Cout % 4 || p.H % KH_TH || p.W % KH_TW || p.B <= 0) return false;
   if (p.C0 % 32 || p.C1 % 32 || p.C0 + p.C1 <= 0) return false;

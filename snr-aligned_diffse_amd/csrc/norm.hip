@@ -14,6 +14,8 @@
 // per-(b, c) scale / shift.
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 template <typename T> struct VecT;
@@ -108,16 +110,32 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const Tin* src0, int C0, 
   const int C = C0 + C1;
   const int b = blockIdx.y;
   const int tid = threadIdx.x;
-  extern __shared__ __attribute__((aligned(16))) float sc[];  // scale[C], shift[C]
+  extern __shared__ __attribute__((aligned(16))) double gap_red[];  // [C][2] folded channel sums, then scale / shift
+  double* const red = gap_red;
+  float* const sc = (float*)(red + 2 * C);                         // scale[C], shift[C]
   if (sums) {
+    // per channel: the SNRSE_STAT_SLOTS partial sums (independent 16-B loads), then per group from LDS
+    for (int c = tid; c < C; c += 256) {
+      const double* st = c < C0 ? sums + stat_idx(b, 0, c, C0) : sums1 + stat_idx(b, 0, c - C0, C1);
+      const size_t sstride = 2 * (size_t)(c < C0 ? C0 : C1);
+      double s = 0.0, ss = 0.0;
+#pragma unroll
+      for (int k = 0; k < SNRSE_STAT_SLOTS; ++k) {
+        s += st[k * sstride];
+        ss += st[k * sstride + 1];
+      }
+      red[2 * c] = s;
+      red[2 * c + 1] = ss;
+    }
+    __syncthreads();
     const int cg = C / groups;
     const double cnt = (double)cg * H * W;
     for (int c = tid; c < C; c += 256) {
       const int g = c / cg;
       double s = 0.0, ss = 0.0;
       for (int k = g * cg; k < (g + 1) * cg; ++k) {
-        if (k < C0) stat_fold(sums, b, k, C0, s, ss);
-        else stat_fold(sums1, b, k - C0, C1, s, ss);
+        s += red[2 * k];
+        ss += red[2 * k + 1];
       }
       const double mean = s / cnt;
       double var = ss / cnt - mean * mean;
@@ -136,6 +154,50 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const Tin* src0, int C0, 
   const int LP = C / V;
   const int total = opix_per_blk * LP;
   const int op0 = blockIdx.x * opix_per_blk;
+  if constexpr (MODE == MODE_NONE && sizeof(Tout) == sizeof(Tin)) {
+    // elementwise: UNR vectors' loads in flight before any is transformed (a load-use chain per vector held
+    // the small-level GroupNorm launches at ~13 us); bf16 takes the fast SiLU as gn_act does, fp32 the exact one
+    constexpr int UNR = 4;
+    const int HWo = Ho * Wo;
+    const int tot = min(opix_per_blk, HWo - op0) * LP;
+    for (int base = tid; base < tot; base += 256 * UNR) {
+      u32x4 raw[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int idx = base + 256 * u;
+        if (idx < tot) {
+          const int op = op0 + idx / LP, c = (idx % LP) * V;
+          raw[u] = *(const u32x4*)(c < C0 ? src0 + ((size_t)b * HWo + op) * C0 + c
+                                          : src1 + ((size_t)b * HWo + op) * C1 + (c - C0));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int idx = base + 256 * u;
+        if (idx < tot) {
+          const int op = op0 + idx / LP, c = (idx % LP) * V;
+          float x[V];
+          if constexpr (sizeof(Tin) == 2) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              x[2 * i] = __uint_as_float(raw[u][i] << 16);
+              x[2 * i + 1] = __uint_as_float(raw[u][i] & 0xffff0000u);
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = __uint_as_float(raw[u][i]);
+          }
+#pragma unroll
+          for (int i = 0; i < V; ++i) {
+            const float y = fmaf(x[i], sc[c + i], sc[C + c + i]);
+            x[i] = act ? (sizeof(Tin) == 2 ? silu(y) : silu_exact(y)) : y;
+          }
+          store_vec<Tout>(out + ((size_t)b * HWo + op) * C + c, x);
+        }
+      }
+    }
+    return;
+  }
   for (int idx = tid; idx < total; idx += 256) {
     const int op = op0 + idx / LP;
     if (op >= Ho * Wo) break;
@@ -309,10 +371,15 @@ static int launch_apply(const void* src0, int C0, const void* src1, int C1, int 
   const int Wo = mode == MODE_DOWN ? W / 2 : (mode == MODE_UP ? 2 * W : W);
   const int V = VecT<Tin>::N;
   const int LP = C / V;
-  int opb = (4 * 256) / LP;
+  // one 16-B output vector per thread: the 4-channel pyramid FIRs (ncsnpp.py:318, 359) ran 4 pixels x 16 taps
+  // per thread at 1024 px per block (up to 35 us per launch at 0.3 of HBM, profiles/r05a_c2_dispatch_shapes.jsonl).
+  // With a GroupNorm every block folds its image's statistics first: at most 8 blocks per image then (the small
+  // levels, where one launch replaces gn_scale_shift + gn_act; snrse/ops.py gn_apply)
+  int opb = 256 / LP;
   if (opb < 1) opb = 1;
+  if (sums) opb = std::max(opb, std::min((Ho * Wo + 7) / 8, 16 * 256 / LP));  // <= 8 folds per image, 16 vectors per thread
   dim3 grid((Ho * Wo + opb - 1) / opb, B);
-  const size_t lds = sizeof(float) * 2 * C;
+  const size_t lds = sizeof(double) * 2 * C + sizeof(float) * 2 * C;
 #define SNRSE_APPLY(MODE_)                                                                          \
   hipLaunchKernelGGL((gn_apply_kernel<Tin, Tout, MODE_>), grid, dim3(256), lds, stream, (const Tin*)src0, \
                      C0, (const Tin*)src1, C1, H, W, sums, sums1, gamma, beta, groups, eps, act, (Tout*)out, opb)

@@ -25,13 +25,17 @@ namespace {
 
 constexpr float kTwoPi = 6.28318530717958647692f;
 
+// snrse_temb_mlp: one block (8 waves) per utterance.  Each wave owns 64 output rows in chunks of 16: a row's
+// weights are read as one coalesced 1-2 KB line set (lane = 4 or 8 consecutive inputs), the 16 per-lane partial
+// dot products are reduced by bfly_sum.  Every block streams all of W1 and W2 through its CU (~44 us at B = 32);
+// the network executor takes the row-parallel pair snrse_temb_gfp_dense + snrse_temb_dense instead.
 __global__ __launch_bounds__(512) void temb_mlp_kernel(const float* t, const float* Wg, const float* W1,
                                                        const float* b1, const float* W2, const float* b2,
                                                        float* temb, int nf) {
   // nf = 128: e[256], h[512], out[512]
-  __shared__ float e[256];
-  __shared__ float h[512];
-  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) float e[256];
+  __shared__ __attribute__((aligned(16))) float h[512];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float lt = logf(t[b]);
   if (tid < nf) {
     const float pr = lt * Wg[tid] * kTwoPi;
@@ -40,64 +44,137 @@ __global__ __launch_bounds__(512) void temb_mlp_kernel(const float* t, const flo
   }
   __syncthreads();
   {
-    float acc = b1[tid];
-    const float* w = W1 + (size_t)tid * 2 * nf;
-    for (int k = 0; k < 2 * nf; ++k) acc = fmaf(w[k], e[k], acc);
-    h[tid] = silu_exact(acc);
+    const f32x4 ev = *(const f32x4*)(e + 4 * lane);  // 2 nf = 256 = 64 lanes x 4
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int j0 = wid * 64 + c * 16;
+      float pp[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) pp[r] = dot4(*(const f32x4*)(W1 + (size_t)(j0 + r) * 2 * nf + 4 * lane), ev);
+      const float v = bfly_sum<16>(pp, lane);
+      if (lane < 16) h[j0 + lane] = silu_exact(v + b1[j0 + lane]);
+    }
   }
   __syncthreads();
   {
-    float acc = b2[tid];
-    const float* w = W2 + (size_t)tid * 4 * nf;
-    for (int k = 0; k < 4 * nf; ++k) acc = fmaf(w[k], h[k], acc);
-    temb[(size_t)b * 4 * nf + tid] = acc;
+    const f32x4 h0 = *(const f32x4*)(h + 8 * lane), h1 = *(const f32x4*)(h + 8 * lane + 4);  // 4 nf = 512
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int j0 = wid * 64 + c * 16;
+      float pp[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float* w = W2 + (size_t)(j0 + r) * 4 * nf + 8 * lane;
+        pp[r] = dot4(*(const f32x4*)w, h0) + dot4(*(const f32x4*)(w + 4), h1);
+      }
+      const float v = bfly_sum<16>(pp, lane);
+      if (lane < 16) temb[(size_t)b * 4 * nf + j0 + lane] = v + b2[j0 + lane];
+    }
   }
 }
 
-// out[b][r] = W[r] . silu(temb[b]) + bias[r];  block: 256 threads = 4 waves, 16 rows per wave
-// out[b][r] = bias[r] + sum_d W[r][d] * silu(temb[b][d]).  Block = 4 waves x 64 rows (lane = row);
-// wave w accumulates images w, w+4, ...; W is read in 64-wide d chunks straight into registers
-// (16-B loads per lane), SiLU(temb) is staged in LDS and read as wave-uniform broadcasts.
-__global__ __launch_bounds__(256) void temb_dense_kernel(const float* temb, const float* W, const float* bias,
-                                                         float* out, int B, int R, int D) {
-  extern __shared__ __attribute__((aligned(16))) float st[];  // [B][D] silu(temb)
+// Row-parallel dense layer over a batch of <= 32 utterances, the time-embedding path (ncsnpp.py:256-275,
+// layerspp.py:264-265):  out[b][r] = act_out(bias[r] + sum_d W[r][d] * in_b[d]),  D <= 512, where in_b is
+//   IN 0: x[b] as given, IN 1: silu(x[b]) (the Dense_0 input), IN 2: the Gaussian-Fourier projection of t[b]
+//   ([sin, cos](2 pi log(t) W_gfp), nf = D / 2 frequencies); act_out = silu for OUT 1.
+// Block = 4 waves; the [32][512] input table is staged in LDS.  A wave requests its kDenseRowsPerWave weight
+// rows up front as coalesced 2 KB lines (lane = 8 consecutive d), forms the 2 x 32 per-lane partial dot
+// products of each row pair against every utterance's LDS row and reduces them with one 64-wide bfly_sum:
+// lane l ends with row l / 32, utterance l % 32.  Every launch reads each weight row once, spread over the
+// chip.  (The previous forms -- an MLP block per utterance streaming all 1.5 MB of W1, W2 through one CU, and
+// a lane-per-row Dense_0 table -- ran ~60 and ~68 us per launch, profiles/r05a_c2_dispatch_shapes.jsonl.)
+constexpr int kDenseRowsPerWave = 8;
+template <int IN, int OUT>
+__global__ __launch_bounds__(256) void temb_dense_kernel(const float* x, const float* t, const float* Wg,
+                                                         const float* W, const float* bias, float* out, int B, int R,
+                                                         int D) {
+  extern __shared__ __attribute__((aligned(16))) float st[];  // [32][512] input rows, zero beyond (B, D)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int i = tid; i < B * D; i += 256) st[i] = silu_exact(temb[i]);
-  __syncthreads();
-  const int r = blockIdx.x * 64 + lane;
-  const bool rok = r < R;
-  float acc[8];
+  // staging: all of a thread's loads issued before any is used (a load-use chain per element held every launch
+  // of this kernel near 30-45 us whatever its size)
+  if constexpr (IN == 2) {
+    const int nf = D >> 1;
+    for (int i = tid; i < 32 * 512; i += 256) {
+      const int bb = i >> 9, d = i & 511;
+      if (bb >= B || d >= 2 * nf) st[i] = 0.f;
+    }
+#pragma unroll 4
+    for (int i = tid; i < B * nf; i += 256) {
+      const int bb = i / nf, k = i - bb * nf;
+      float sn, cs;
+      sincosf(logf(t[bb]) * Wg[k] * kTwoPi, &sn, &cs);
+      st[bb * 512 + k] = sn;
+      st[bb * 512 + nf + k] = cs;
+    }
+  } else {
+    constexpr int NQ = 32 * 512 / 4 / 256;  // f32x4 pieces per thread
+    f32x4 v[NQ];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-  for (int d0 = 0; d0 < D; d0 += 64) {
-    f32x4 w[16];
+    for (int j = 0; j < NQ; ++j) {
+      const int q = tid + 256 * j, bb = q >> 7, d = (q & 127) * 4;
+      v[j] = (bb < B && d < D) ? *(const f32x4*)(x + (size_t)bb * D + d) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
-    for (int q = 0; q < 16; ++q)
-      w[q] = (rok && d0 + 4 * q < D) ? *(const f32x4*)(W + (size_t)r * D + d0 + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NQ; ++j) {
+      const int q = tid + 256 * j, bb = q >> 7, d = (q & 127) * 4;
+      f32x4 a = v[j];
+      if constexpr (IN == 1) {
+        if (bb < B && d < D) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int b = wid + 4 * k;
-      if (b < B) {
-        const float* sb = st + b * D + d0;
-        float a = acc[k];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          if (d0 + 4 * q < D) {
-            const f32x4 sv = *(const f32x4*)(sb + 4 * q);
-            a = fmaf(w[q][0], sv[0], fmaf(w[q][1], sv[1], fmaf(w[q][2], sv[2], fmaf(w[q][3], sv[3], a))));
-          }
+          for (int e = 0; e < 4; ++e) a[e] = silu_exact(a[e]);
         }
-        acc[k] = a;
       }
+      *(f32x4*)(st + bb * 512 + d) = a;
     }
   }
-  if (rok) {
+  __syncthreads();
+  const int d0 = 8 * lane;
+  const bool dok = d0 < D;  // D % 4 == 0 and D <= 512: a lane's 8 inputs are all valid or (second half) zero
+  const bool dok2 = d0 + 4 < D;
+  const int rw0 = (blockIdx.x * 4 + wid) * kDenseRowsPerWave;
+  f32x4 wall[kDenseRowsPerWave][2];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int b = wid + 4 * k;
-      if (b < B) out[(size_t)b * R + r] = acc[k] + bias[r];
+  for (int q = 0; q < kDenseRowsPerWave; ++q) {
+    const int r = min(rw0 + q, R - 1);
+    const float* wp = W + (size_t)r * D + d0;
+    wall[q][0] = dok ? *(const f32x4*)wp : f32x4{0.f, 0.f, 0.f, 0.f};
+    wall[q][1] = dok2 ? *(const f32x4*)(wp + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int rp = 0; rp < kDenseRowsPerWave; rp += 2) {
+    const int r0 = rw0 + rp;
+    if (r0 >= R) break;  // wave-uniform
+    float pp[64];
+#pragma unroll
+    for (int bb = 0; bb < 32; ++bb) {
+      const f32x4 s0 = *(const f32x4*)(st + bb * 512 + d0), s1 = *(const f32x4*)(st + bb * 512 + d0 + 4);
+      pp[bb] = dot4(wall[rp][0], s0) + dot4(wall[rp][1], s1);
+      pp[32 + bb] = dot4(wall[rp + 1][0], s0) + dot4(wall[rp + 1][1], s1);
+    }
+    const float v = bfly_sum<64>(pp, lane);
+    const int r = r0 + (lane >> 5), bb = lane & 31;
+    if (r < R && bb < B) {
+      const float y = v + bias[r];
+      out[(size_t)bb * R + r] = OUT == 1 ? silu_exact(y) : y;
     }
   }
+}
+
+template <int IN, int OUT>
+int launch_dense(const float* x, const float* t, const float* Wg, const float* W, const float* bias, float* out, int B,
+                 int R, int D, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute((const void*)temb_dense_kernel<IN, OUT>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 32 * 512 * 4);
+  SNRSE_RET(attr);
+  const int rows_per_block = 4 * kDenseRowsPerWave;
+  for (int b0 = 0; b0 < B; b0 += 32) {  // the LDS table holds 32 utterances
+    const int nb = std::min(32, B - b0);
+    hipLaunchKernelGGL((temb_dense_kernel<IN, OUT>), dim3((R + rows_per_block - 1) / rows_per_block), dim3(256),
+                       sizeof(float) * 32 * 512, s, x ? x + (size_t)b0 * D : nullptr, t ? t + b0 : nullptr, Wg, W,
+                       bias, out + (size_t)b0 * R, nb, R, D);
+    SNRSE_LAUNCH_CHECK();
+  }
+  return 0;
 }
 
 // One lane per 16-byte chunk of a pixel's 64-channel im2col row (NCH = 64 / VEC chunks per pixel),
@@ -707,19 +784,16 @@ extern "C" int snrse_temb_mlp(const float* t, const float* Wg, const float* W1, 
   return (int)hipGetLastError();
 }
 
+extern "C" int snrse_temb_gfp_dense(const float* t, const float* Wg, const float* W1, const float* b1, float* out,
+                                    int B, int nf, hipStream_t s) {
+  if (nf <= 0 || 2 * nf > 512 || nf % 2 || B <= 0 || !t || !Wg || !W1 || !b1 || !out) return SNRSE_EINVAL;
+  return launch_dense<2, 0>(nullptr, t, Wg, W1, b1, out, B, 4 * nf, 2 * nf, s);
+}
+
 extern "C" int snrse_temb_dense(const float* temb, const float* W, const float* bias, float* out, int B, int R,
                                 int D, hipStream_t s) {
   if (D > 512 || D % 4 || B <= 0 || R <= 0) return SNRSE_EINVAL;
-  // the kernel stages a [b][D] table of SiLU(temb) in LDS: launch over batch chunks of at most 32
-  // utterances (64 KB at D = 512) so any batch size works
-  const int chunk = std::max(1, std::min(32, (64 * 1024) / (4 * D)));
-  for (int b0 = 0; b0 < B; b0 += chunk) {
-    const int nb = std::min(chunk, B - b0);
-    hipLaunchKernelGGL(temb_dense_kernel, dim3((R + 63) / 64), dim3(256), sizeof(float) * nb * D, s,
-                       temb + (size_t)b0 * D, W, bias, out + (size_t)b0 * R, nb, R, D);
-    SNRSE_LAUNCH_CHECK();
-  }
-  return 0;
+  return launch_dense<1, 0>(temb, nullptr, nullptr, W, bias, out, B, R, D, s);
 }
 
 extern "C" int snrse_input_conv(snrse_ctx* ctx, const void* x, const void* y, int B, int H, int W, const void* wgt, const float* bias,

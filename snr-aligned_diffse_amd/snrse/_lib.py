@@ -33,6 +33,7 @@ SIGNATURES = {
     "snrse_attention": [_vp, _vp, _i, _i, _i, _i, _vp],
     "snrse_temb_mlp": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp],
     "snrse_temb_dense": [_vp, _vp, _vp, _vp, _i, _i, _i, _vp],
+    "snrse_temb_gfp_dense": [_vp, _vp, _vp, _vp, _vp, _i, _i, _vp],
     "snrse_input_pack": [_vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp],
     "snrse_score_update": [_vp, _i, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp],
     "snrse_sde_update": [_vp, _vp, _vp, _vp, _u64, _u64, _vp, _i, _i, _vp, _vp, _vp],

@@ -232,7 +232,7 @@ def probe_read(max_calls, dev=None, all_threads=False):
 
 KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 3: "conv_x3_kernel", 4: "conv_x3h_kernel",
            5: "conv_halo5_kernel",
-           10: "conv_head_kernel", 11: "conv_head_x3_kernel"}
+           10: "conv_head_kernel", 11: "conv_head_x3_kernel", 14: "conv_head_small_kernel"}
 
 
 def kernel_name(gen):
@@ -268,14 +268,18 @@ def x3h_ok(x, ksize, cout):
 
 
 def head_ok(x, split=False):
-    """True when a 3x3 conv of x with Cout <= 16 and f32 output (the pyramid heads) takes the halo-staged
-    head kernel, which accepts a fused GroupNorm (gn=): bf16 x, or f32 x with split weights (split=True,
-    the fp32x3 mode's conv_head_x3_kernel)."""
+    """True when a 3x3 conv of x with Cout = 4 and f32 output (the pyramid heads) takes a head kernel that
+    accepts a fused GroupNorm (gn=): the halo-staged head (bf16 x, or f32 x with split weights: split=True, the
+    fp32x3 mode's conv_head_x3_kernel; H % 8 == 0, W % 32 == 0), or for bf16 x with C % 256 == 0 the
+    wave-per-8-pixels head of the other image sizes (option head_small, snrse_conv2d)."""
     B, H, W, C = x.shape
+    if _opt(x, "conv_variant") == 1:
+        return False
     dt_ok = x.dtype == torch.bfloat16 or (split and x.dtype == torch.float32)
     # channels: the C-ABI's K-tile (64 bf16 / 32 f32 channels, snrse_conv2d)
-    return dt_ok and H % 8 == 0 and W % 32 == 0 and C % (64 if x.dtype == torch.bfloat16 else 32) == 0 and \
-        _opt(x, "conv_variant") != 1
+    if dt_ok and H % 8 == 0 and W % 32 == 0 and C % (64 if x.dtype == torch.bfloat16 else 32) == 0:
+        return True
+    return x.dtype == torch.bfloat16 and C % 256 == 0 and _opt(x, "head_small") != 0
 
 
 def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):
@@ -388,6 +392,7 @@ def gn_stats(src0, src1=None):
 
 
 MODES = {"none": 0, "down": 1, "up": 2}
+GN_FUSED_MAX_HW = 512  # gn_apply: images up to this many pixels take the single fold + apply launch
 
 
 def gn_apply(src0, src1=None, sums=None, gamma=None, beta=None, act=True, mode="none", groups=None, eps=1e-6,
@@ -400,7 +405,10 @@ def gn_apply(src0, src1=None, sums=None, gamma=None, beta=None, act=True, mode="
     C1 = 0 if src1 is None else src1.shape[3]
     C = C0 + C1
     m = MODES[mode]
-    if sums is not None and (m == 0 or resample_ok(src0)):
+    # small images (the 16 x 32 .. 4 x 8 levels of C2): ONE launch that folds the statistics per block (at most
+    # 4 blocks per image) and applies, instead of gn_scale_shift + gn_act -- two launch-floor kernels
+    small = m == 0 and H * W <= GN_FUSED_MAX_HW
+    if sums is not None and (m == 0 or resample_ok(src0)) and not small:
         # the per-(b, c) affine once (snrse_gn_scale_shift), then the elementwise / LDS-tiled apply: no
         # per-block re-fold of the slotted statistics (the fp32 gn_apply pass ran at ~0.2 of HBM peak that way)
         scale, shift = gn_scale_shift(sums, gamma, beta, H * W, sums1=sums1, groups=groups, eps=eps)
@@ -468,12 +476,21 @@ def attention(qkv, C=256):
     return out
 
 
-def temb_mlp(t, Wg, W1, b1, W2, b2):
+def temb_mlp(t, Wg, W1, b1, W2, b2, fused=False):
+    """temb [B, 4 nf] (ncsnpp.py:256-275): two row-parallel launches, snrse_temb_gfp_dense (W1 gfp(t) + b1) then
+    snrse_temb_dense (W2 silu(.) + b2); fused=True: the one-launch snrse_temb_mlp (a block per utterance)."""
     _dev(t, Wg, W1, b1, W2, b2)
     B = t.shape[0]
     out = torch.empty(B, W2.shape[0], device=t.device, dtype=torch.float32)
-    _lib.call("snrse_temb_mlp", t.data_ptr(), Wg.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
-              b2.data_ptr(), out.data_ptr(), B, Wg.shape[0], _stream())
+    if fused:
+        _lib.call("snrse_temb_mlp", t.data_ptr(), Wg.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
+                  b2.data_ptr(), out.data_ptr(), B, Wg.shape[0], _stream())
+        return out
+    a = torch.empty(B, W1.shape[0], device=t.device, dtype=torch.float32)
+    _lib.call("snrse_temb_gfp_dense", t.data_ptr(), Wg.data_ptr(), W1.data_ptr(), b1.data_ptr(), a.data_ptr(), B,
+              Wg.shape[0], _stream())
+    _lib.call("snrse_temb_dense", a.data_ptr(), W2.data_ptr(), b2.data_ptr(), out.data_ptr(), B, W2.shape[0],
+              W2.shape[1], _stream())
     return out
 
 

@@ -244,7 +244,7 @@ def test_upfirdn2d_half_double(gpu, dtype, atol):
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
-@pytest.mark.parametrize("L", [128, 37, 512])
+@pytest.mark.parametrize("L", [128, 37, 512, 100])
 def test_attention_core(gpu, dt, L):
     from snrse import ops
     dtype, tol = DT[dt]
@@ -294,6 +294,30 @@ def test_ncsnpp_full_golden(gpu, sd_ncsnpp, dt):
     assert err < (1e-4 if dt == "f32" else 2e-2), err
     if dt == "f32":
         assert abs_rms(out, g["out"][:, 0]) < 1e-4
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_temb_golden(gpu, sd_ncsnpp, fused):
+    """Time embedding (ncsnpp.py:256-275) against the reference-generated golden: the row-parallel pair
+    snrse_temb_gfp_dense + snrse_temb_dense the executor runs, and the one-launch snrse_temb_mlp; then the
+    Dense_0 table of every ResBlock (layerspp.py:264-265) against float64 for a 40-utterance batch (two LDS
+    batches of the table kernel)."""
+    from snrse import ncsnpp, ops
+    g = golden("ncsnpp_full.npz")
+    net = ncsnpp.NCSNppHIP(sd_ncsnpp, dtype=torch.float32)
+    W = net.W
+    t = torch.tensor([0.5, 0.8], device=gpu)
+    te = ops.temb_mlp(t, W["gfp"], W["l1w"], W["l1b"], W["l2w"], W["l2b"], fused=fused)
+    np.testing.assert_allclose(te.cpu().numpy(), g["temb"], rtol=1e-5, atol=1e-5)
+    tb = torch.rand(40, device=gpu) * 0.9 + 0.05
+    te = ops.temb_mlp(tb, W["gfp"], W["l1w"], W["l1b"], W["l2w"], W["l2b"], fused=fused)
+    e = torch.log(tb.double())[:, None] * W["gfp"].double()[None, :] * 2 * math.pi
+    e = torch.cat([torch.sin(e), torch.cos(e)], 1)
+    ref = F.silu(e @ W["l1w"].double().t() + W["l1b"].double()) @ W["l2w"].double().t() + W["l2b"].double()
+    assert rel(te, ref) < 1e-5
+    tab = ops.temb_dense(te, W["dense_w"], W["dense_b"])
+    ref_tab = F.silu(te.double()) @ W["dense_w"].double().t() + W["dense_b"].double()
+    assert rel(tab, ref_tab) < 1e-5
 
 
 def test_stft_istft_golden(gpu):
@@ -617,6 +641,51 @@ def test_conv_splitk_small_levels(gpu, case):
     assert rel(outs[1][0].float(), outs[0][0].float()) < tol
 
 
+@pytest.mark.parametrize("B,C0,C1,Csc,H,W", [(32, 256, 0, 0, 16, 32), (8, 256, 256, 0, 8, 16), (16, 256, 0, 256, 8, 16),
+                                             (3, 256, 256, 512, 4, 8), (5, 256, 0, 0, 15, 20)])
+def test_glds_small_levels(gpu, B, C0, C1, Csc, H, W):
+    """The LDS-DMA GEMM on the 16 x 32 .. 4 x 8 levels (layerspp.py:244-276) against fp64: 3x3 conv over a
+    concatenated input, the 1x1 shortcut as extra K, bias + temb + residual + scale and statistics (wave tiles
+    spanning images where H*W < 64), with and without K splits."""
+    from snrse import ops
+    cout = 256
+    x = torch.from_numpy(fnormal("t.gv.x", (B, C0 + C1, H, W))).bfloat16().float()
+    w = (torch.from_numpy(fnormal("t.gv.w", (cout, C0 + C1, 3, 3))) / 68).bfloat16().float()
+    b = torch.from_numpy(fnormal("t.gv.b", (cout,)))
+    temb = torch.from_numpy(fnormal("t.gv.t", (B, 300)))
+    r = torch.from_numpy(fnormal("t.gv.r", (B, cout, H, W))).bfloat16().float()
+    ref = F.conv2d(x.double(), w.double(), b.double(), padding=1) + temb[:, 8:8 + cout, None, None].double()
+    kw = {}
+    if Csc:
+        xs = torch.from_numpy(fnormal("t.gv.s", (B, Csc, H, W))).bfloat16().float()
+        ws = (torch.from_numpy(fnormal("t.gv.ws", (cout, Csc))) / 20).bfloat16().float()
+        ref = ref + torch.einsum("bchw,oc->bohw", xs.double(), ws.double())
+        kw = dict(sc=nhwc(xs).to(gpu, torch.bfloat16), sc_wgt=ws.to(gpu, torch.bfloat16).contiguous())
+    else:
+        kw = dict(res=nhwc(r).to(gpu, torch.bfloat16))
+        ref = ref + r.double()
+    ref = ref * 0.5
+    rd = nhwc(ref)
+    st_ref = torch.stack([rd.sum((1, 2)), (rd * rd).sum((1, 2))], -1).to(gpu)
+    xg = nhwc(x).to(gpu, torch.bfloat16)
+    wp = w.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu, torch.bfloat16).contiguous()
+    outs = []
+    for sk in (1, 0):
+        ops.set_option("splitk", sk)
+        try:
+            st = ops.new_stats(B, cout)
+            o = ops.conv2d(xg[..., :C0].contiguous(), wp, 3, cout, bias=b.to(gpu),
+                           src1=xg[..., C0:].contiguous() if C1 else None, temb=temb.to(gpu), temb_off=8,
+                           out_scale=0.5, stats=st, **kw)
+            assert ops.kernel_name(ops.get_option("last_kernel")) == "conv_glds_kernel"
+        finally:
+            ops.set_option("splitk", 1)
+        assert rel(nchw(o.float()), ref) < 1e-2
+        assert rel(ops.fold_stats(st), st_ref) < 1e-4
+        outs.append(o.float())
+    assert rel(outs[1], outs[0]) < 1e-2
+
+
 @pytest.mark.parametrize("shape", [(2, 128, 8, 64), (1, 256, 8, 128), (2, 128, 16, 32), (1, 256, 24, 96),
                                    (2, 192, 16, 64), (1, 64, 8, 32)])
 def test_conv_head_fused_groupnorm(gpu, shape):
@@ -641,6 +710,66 @@ def test_conv_head_fused_groupnorm(gpu, shape):
     assert ops.kernel_name(ops.get_option("last_kernel")) == "conv_head_kernel"
     assert out.dtype == torch.float32
     assert rel(nchw(out), ref) < 1e-2
+
+
+@pytest.mark.parametrize("shape,act,small", [((32, 256, 4, 8), True, 1), ((32, 256, 8, 16), True, 1),
+                                             ((3, 512, 5, 11), True, 1), ((2, 256, 7, 3), False, 1),
+                                             ((4, 256, 16, 32), True, 2), ((2, 256, 8, 16), None, 1)])
+def test_conv_head_small(gpu, shape, act, small):
+    """Pyramid heads of the small levels (ncsnpp.py:348-366: the 8 x 16 and 4 x 8 levels of C2, which the tiled
+    head cannot take) through the wave-per-8-pixels head with the GroupNorm(+SiLU) fused (act None: no norm);
+    ragged widths and heights, 2 channel passes, and option head_small 2 on a tiled-head shape."""
+    from snrse import ops
+    B, C, H, W = shape
+    x = (torch.from_numpy(fnormal("t.hs.x", (B, C, H, W))) * 1.5 + 0.2).bfloat16().float()
+    w = (torch.from_numpy(fnormal("t.hs.w", (4, C, 3, 3))) / 48).bfloat16().float()
+    b = torch.from_numpy(fnormal("t.hs.b", (4,)))
+    r = torch.from_numpy(fnormal("t.hs.r", (B, 4, H, W)))
+    g = torch.from_numpy(fnormal("t.hs.g", (C,))) * 0.1 + 1
+    be = torch.from_numpy(fnormal("t.hs.be", (C,))) * 0.1
+    if act is None:
+        a = x.double()
+    else:
+        a = F.group_norm(x.double(), min(C // 4, 32), g.double(), be.double(), eps=1e-6)
+        a = F.silu(a) if act else a
+    ref = (F.conv2d(a, w.double(), b.double(), padding=1) + r.double()) * 0.75
+    xg = nhwc(x).to(gpu, torch.bfloat16)
+    gn = None
+    if act is not None:
+        sums, _ = ops.gn_stats(xg)
+        gn = ops.gn_scale_shift(sums, g.to(gpu), be.to(gpu), H * W)
+    wp = torch.cat([w.permute(0, 2, 3, 1).reshape(4, -1), torch.zeros(12, 9 * C)]).to(gpu, torch.bfloat16).contiguous()
+    ops.set_option("head_small", small)
+    try:
+        assert ops.head_ok(xg)
+        out = ops.conv2d(xg, wp, 3, 4, bias=b.to(gpu), res=nhwc(r).to(gpu), out_f32=True, gn=gn,
+                         gn_act=bool(act), out_scale=0.75)
+        assert ops.kernel_name(ops.get_option("last_kernel")) == "conv_head_small_kernel"
+    finally:
+        ops.set_option("head_small", 1)
+    assert out.dtype == torch.float32
+    assert rel(nchw(out), ref) < 1e-3
+
+
+@pytest.mark.parametrize("shape", [(32, 256, 4, 8), (6, 256, 2, 4), (5, 128, 4, 4), (3, 256, 3, 5)])
+def test_glds_multi_image_tile_statistics(gpu, shape):
+    """A 1x1 GEMM on images smaller than a wave tile (H*W < 64: the NIN_3 of the 4 x 8 mid-block attention,
+    layerspp.py:92) reduces its GroupNorm statistics per image run; they must equal the per-image sums."""
+    from snrse import ops
+    B, C, H, W = shape
+    x = (torch.from_numpy(fnormal("t.gm.x", (B, C, H, W)))).bfloat16().float()
+    w = (torch.from_numpy(fnormal("t.gm.w", (256, C))) / 16).bfloat16().float()
+    bias = torch.from_numpy(fnormal("t.gm.b", (256,)))
+    ref = torch.einsum("bchw,oc->bohw", x.double(), w.double()) + bias.double()[None, :, None, None]
+    xg = nhwc(x).to(gpu, torch.bfloat16)
+    st = ops.new_stats(B, 256)
+    out = ops.conv2d(xg, w.to(gpu, torch.bfloat16).contiguous(), 1, 256, bias=bias.to(gpu), stats=st)
+    assert ops.kernel_name(ops.get_option("last_kernel")) == "conv_glds_kernel"
+    assert rel(nchw(out.float()), ref) < 1e-2
+    # the epilogue sums the fp32 results before their bf16 rounding: compare with the exact GEMM's
+    rd = nhwc(ref)
+    st_ref = torch.stack([rd.sum((1, 2)), (rd * rd).sum((1, 2))], -1).to(gpu)
+    assert rel(ops.fold_stats(st), st_ref) < 1e-4
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])

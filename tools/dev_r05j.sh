@@ -1,0 +1,10 @@
+# r05j: tail launches (multi-image GEMM statistics, small-level pyramid heads, temb kernels, pyramid FIR grid):
+# new + affected GPU tests, smoke, micro-benchmarks, the default line, a traced line with per-dispatch shapes
+O=$PWD/gpurun_out/r05j
+R=$GRAFT_REPO_ROOT
+bash tools/gpu_step.sh $O \
+ "tests:::400:::cd $R && python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_c2_path.py tests/test_gpu_x3.py -m gpu -x -q --timeout 300 --timeout-method thread" \
+ "smoke:::200:::cd $R && python -u -c 'import __graft_entry__ as g; g.smoke()'" \
+ "tail:::200:::cd $R && python -u tools/tail_bench.py > $O/tail_bench.jsonl" \
+ "bench:::300:::cd $R && python -u bench.py --no-cpu-baseline > $O/bench.json" \
+ "trace:::400:::cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --output-format csv -d $O/trace -o run -- python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-parity-mode --no-probe --no-parity > $O/bench_traced.json && python3 $R/tools/dispatch_shapes.py $O/trace/run_kernel_trace.csv > $O/dispatch_shapes.jsonl && rm -f $O/trace/run_kernel_trace.csv"
