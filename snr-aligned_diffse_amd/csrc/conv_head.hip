@@ -20,40 +20,41 @@ constexpr int KH_HJ = (KH_HROWS + 63) / 64;    // halo rows per thread: (tid >> 
 constexpr int KH_HALO = KH_HROWS * 64;         // 21760 B
 constexpr int KH_WP = 9 * 16 * 4;              // 16-B weight pieces of one chunk: 9 taps x 16 co x 4
 constexpr int KH_WJ = (KH_WP + 255) / 256;     // per thread (3)
-constexpr int KH_LDS = KH_HALO + 9 * 1024;     // + 9 taps x 16 co x 64 B = 34560 B
+constexpr int KH_MAXC = 1024;                  // input channels the LDS GroupNorm table holds
+constexpr int KH_LDS = KH_HALO + 9 * 1024 + 2 * KH_MAXC * 4;  // + 9 taps x 16 co x 64 B + [2][C] affine
 
 SNRSE_DEV int kh_swz(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >> 1) & 3)) << 4); }
 
-#define KH_LOAD(C_)                                                                                            \
+#define KH_LOAD_H(C_, HV)                                                                                      \
   do {                                                                                                         \
-    const int ch_ = (C_) * 32;                                                                                 \
+    const bool in_ = (C_) < nc;                                                                                \
+    const int ch_ = in_ ? (C_) * 32 : 0;                                                                       \
     const bool u1_ = ch_ >= p.C0;                                                                              \
     const __amdgpu_buffer_rsrc_t r_ = u1_ ? make_rsrc(p.src1, p.bytes1) : make_rsrc(p.src0, p.bytes0);         \
     const int cs_ = u1_ ? p.C1 : p.C0, cc_ = (u1_ ? ch_ - p.C0 : ch_) + hcol * 8;                              \
     _Pragma("unroll") for (int j = 0; j < KH_HJ; ++j) {                                                        \
-      const int voff_ = hok[j] ? (hpix[j] * cs_ + cc_) * 2 : (int)0x80000000;                                  \
-      hv[j] = __builtin_amdgcn_raw_buffer_load_b128(r_, voff_, 0, 0);                                          \
+      const int voff_ = (hok[j] && in_) ? (hpix[j] * cs_ + cc_) * 2 : (int)0x80000000;                         \
+      HV[j] = __builtin_amdgcn_raw_buffer_load_b128(r_, voff_, 0, 0);                                          \
     }                                                                                                          \
+  } while (0)
+#define KH_LOAD_W(C_)                                                                                          \
+  do {                                                                                                         \
+    const bool in_ = (C_) < nc;                                                                                \
+    const int ch_ = (C_) * 32;                                                                                 \
     _Pragma("unroll") for (int k = 0; k < KH_WJ; ++k) {                                                        \
       const int pc_ = tid + 256 * k; /* tap (pc >> 6), co ((pc >> 2) & 15), 16-B chunk (pc & 3) */              \
-      const int voff_ = pc_ < KH_WP ? ((((pc_ >> 2) & 15) * K1 + (pc_ >> 6) * Cin + ch_ + (pc_ & 3) * 8) * 2)   \
-                                    : (int)0x80000000;                                                         \
+      const int voff_ = (pc_ < KH_WP && in_) ? ((((pc_ >> 2) & 15) * K1 + (pc_ >> 6) * Cin + ch_ + (pc_ & 3) * 8) * 2) \
+                                             : (int)0x80000000;                                                \
       wv[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, voff_, 0, 0);                                          \
-    }                                                                                                          \
-    if (gn) {                                                                                                  \
-      const float* sp_ = p.gn_scale + (size_t)b * Cin + ch_ + hcol * 8;                                        \
-      const float* hp_ = p.gn_shift + (size_t)b * Cin + ch_ + hcol * 8;                                        \
-      gs0 = *(const f32x4*)sp_;                                                                                \
-      gs1 = *(const f32x4*)(sp_ + 4);                                                                          \
-      gh0 = *(const f32x4*)hp_;                                                                                \
-      gh1 = *(const f32x4*)(hp_ + 4);                                                                          \
-      if (GNM == 2) { /* gn_xform8's prescaled SiLU affine */                                                  \
-        gs0 *= kNegLog2e; gs1 *= kNegLog2e; gh0 *= kNegLog2e; gh1 *= kNegLog2e;                               \
-      }                                                                                                        \
     }                                                                                                          \
   } while (0)
 
-// grid: B * (H / 4) * (W / 64) workgroups of 256.  GNM: 0 no prologue, 1 GroupNorm affine, 2 + SiLU
+// grid: B * (H / 8) * (W / 32) workgroups of 256.  GNM: 0 no prologue, 1 GroupNorm affine, 2 + SiLU.
+// Round 5: the halo of chunk c + 2 is requested as soon as chunk c's registers are in LDS (two register
+// buffers: two chunks of transform + MFMA work of cover instead of one MFMA phase; level 0 in situ 421 -> 390 us,
+// profiles/r05m_c2_dispatch_shapes.jsonl), every chunk issues the same loads (out-of-range offsets past the last
+// chunk load zeros) so the compiler's vmcnt model stays exact, and the GroupNorm affine of the image is staged
+// once in LDS (per-chunk scale / shift registers would have cost the third workgroup per CU).
 #ifndef SNRSE_HEAD_MINB
 #define SNRSE_HEAD_MINB 1  // workgroups per CU the register allocation is bounded for (A/B builds)
 #endif
@@ -62,6 +63,7 @@ __global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvPar
   __shared__ __attribute__((aligned(16))) char smem[KH_LDS];
   char* const halo = smem;
   char* const wsl = smem + KH_HALO;
+  float* const gtab = (float*)(smem + KH_HALO + 9 * 1024);  // [2][Cin] scale, shift (prescaled for GNM 2)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntw = p.W / KH_TW, nth = p.H / KH_TH;
@@ -88,26 +90,58 @@ __global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvPar
     hok[j] = hr < KH_HROWS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
     hpix[j] = (b * p.H + ih) * p.W + iw;
   }
-  u32x4 hv[KH_HJ], wv[KH_WJ];
-  f32x4 gs0 = {1.f, 1.f, 1.f, 1.f}, gs1 = gs0, gh0 = {0.f, 0.f, 0.f, 0.f}, gh1 = gh0;
+  u32x4 hv[KH_HJ], hw[KH_HJ], wv[KH_WJ];
 
   // acc[i]: D[co = 4 lg + e][px = w0 + 16 i + lrow]  (A = weights, B = halo pixels)
   f32x4 acc[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  KH_LOAD(0);
-  for (int c = 0; c < nc; ++c) {
+  // the affine table's loads go first: the in-order vmcnt wait before its LDS stores then leaves the halo
+  // and weight loads behind it in flight
+  float gsc[KH_MAXC / 256], gsh[KH_MAXC / 256];
+  if constexpr (gn) {
+#pragma unroll
+    for (int k = 0; k < KH_MAXC / 256; ++k) {
+      const int i = tid + 256 * k;
+      if (i < Cin) {
+        gsc[k] = p.gn_scale[(size_t)b * Cin + i];
+        gsh[k] = p.gn_shift[(size_t)b * Cin + i];
+      }
+    }
+  }
+  KH_LOAD_H(0, hv);
+  KH_LOAD_W(0);
+  KH_LOAD_H(1, hw);
+  if constexpr (gn) {
+#pragma unroll
+    for (int k = 0; k < KH_MAXC / 256; ++k) {
+      const int i = tid + 256 * k;
+      if (i < Cin) {
+        gtab[i] = GNM == 2 ? gsc[k] * kNegLog2e : gsc[k];  // gn_xform8's prescaled SiLU affine
+        gtab[Cin + i] = GNM == 2 ? gsh[k] * kNegLog2e : gsh[k];
+      }
+    }
+    __syncthreads();
+  }
+  auto step = [&](int c, u32x4 (&h)[KH_HJ]) {
     // registers -> LDS: GroupNorm + SiLU on the halo (rows outside the image stay zero), weights
+    float sc[8], sh[8];
+    if constexpr (gn) {
+      const float* gp = gtab + c * 32 + hcol * 8;
+      const f32x4 s0 = *(const f32x4*)gp, s1 = *(const f32x4*)(gp + 4);
+      const f32x4 t0 = *(const f32x4*)(gp + Cin), t1 = *(const f32x4*)(gp + Cin + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sc[e] = s0[e]; sc[4 + e] = s1[e];
+        sh[e] = t0[e]; sh[4 + e] = t1[e];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < KH_HJ; ++j) {
       const int hr = (tid >> 2) + 64 * j;
       if (j == KH_HJ - 1 && hr >= KH_HROWS) break;
-      u32x4 v = hv[j];
-      if constexpr (gn) {
-        const float sc[8] = {gs0[0], gs0[1], gs0[2], gs0[3], gs1[0], gs1[1], gs1[2], gs1[3]};
-        const float sh[8] = {gh0[0], gh0[1], gh0[2], gh0[3], gh1[0], gh1[1], gh1[2], gh1[3]};
-        v = gn_xform8<GNM>(v, sc, sh, hok[j]);  // rows outside the image: the conv's zero padding
-      }
+      u32x4 v = h[j];
+      if constexpr (gn) v = gn_xform8<GNM>(v, sc, sh, hok[j]);  // rows outside the image: the conv's zero padding
       *(u32x4*)(halo + kh_swz(hr, hcol)) = v;
     }
 #pragma unroll
@@ -115,8 +149,11 @@ __global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvPar
       const int pc = tid + 256 * k;
       if (pc < KH_WP) *(u32x4*)(wsl + (pc >> 6) * 1024 + kh_swz((pc >> 2) & 15, pc & 3)) = wv[k];
     }
+    // both register sets are free again: the next chunk's weights first (the in-order vmcnt wait before their
+    // LDS store then does not wait on the later halo), then the halo two chunks ahead (past the end: zeros)
+    KH_LOAD_W(c + 1);
+    KH_LOAD_H(c + 2, h);
     __syncthreads();
-    if (c + 1 < nc) KH_LOAD(c + 1);
 #pragma unroll
     for (int tp = 0; tp < 9; ++tp) {
       const int dy = tp / 3 - 1, dx = tp % 3 - 1;
@@ -129,6 +166,10 @@ __global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvPar
       }
     }
     __syncthreads();
+  };
+  for (int c = 0; c < nc; c += 2) {  // nc is even: bf16 channels come in 64-channel K-tiles (snrse_conv2d)
+    step(c, hv);
+    step(c + 1, hw);
   }
   // epilogue: lanes with 4 lg < Cout hold channels 4 lg .. 4 lg + 3 of one pixel
   const int co = 4 * lg;
@@ -145,7 +186,8 @@ __global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvPar
     }
   }
 }
-#undef KH_LOAD
+#undef KH_LOAD_H
+#undef KH_LOAD_W
 
 // fp32 form for the split-bf16 parity mode (SNRSE_F32X3): fp32 activations, weights pre-split per 32-element
 // K-tile into 32 hi then 32 lo bf16 (ops.split_weight).  Each halo vector (8 fp32 channels, 2 x 16 B) gets
@@ -408,7 +450,7 @@ int launch_head_small(const ConvParams& p, hipStream_t s) {
 
 bool head_ok(const ConvParams& p) {
   if (p.ksize != 3 || p.Cout > 16 || p.Cout % 4 || p.H % KH_TH || p.W % KH_TW || p.B <= 0) return false;
-  if (p.C0 % 32 || p.C1 % 32 || p.C0 + p.C1 <= 0) return false;
+  if (p.C0 % 32 || p.C1 % 32 || p.C0 + p.C1 <= 0 || p.C0 + p.C1 > KH_MAXC) return false;
   if (p.sc_src || p.temb || p.comb_src || p.stats) return false;
   if (p.out_ld % 4 || (p.res && p.res_ld % 4)) return false;
   const long long lim = 0x7ff00000ll;

@@ -373,11 +373,11 @@ static int launch_apply(const void* src0, int C0, const void* src1, int C1, int 
   const int LP = C / V;
   // one 16-B output vector per thread: the 4-channel pyramid FIRs (ncsnpp.py:318, 359) ran 4 pixels x 16 taps
   // per thread at 1024 px per block (up to 35 us per launch at 0.3 of HBM, profiles/r05a_c2_dispatch_shapes.jsonl).
-  // With a GroupNorm every block folds its image's statistics first: at most 8 blocks per image then (the small
+  // With a GroupNorm every block folds its image's statistics first: at most 16 blocks per image then (the small
   // levels, where one launch replaces gn_scale_shift + gn_act; snrse/ops.py gn_apply)
   int opb = 256 / LP;
   if (opb < 1) opb = 1;
-  if (sums) opb = std::max(opb, std::min((Ho * Wo + 7) / 8, 16 * 256 / LP));  // <= 8 folds per image, 16 vectors per thread
+  if (sums) opb = std::max(opb, std::min((Ho * Wo + 15) / 16, 16 * 256 / LP));  // <= 16 folds per image, 16 vectors per thread
   dim3 grid((Ho * Wo + opb - 1) / opb, B);
   const size_t lds = sizeof(double) * 2 * C + sizeof(float) * 2 * C;
 #define SNRSE_APPLY(MODE_)                                                                          \

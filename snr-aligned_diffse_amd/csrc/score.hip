@@ -74,37 +74,36 @@ __global__ __launch_bounds__(512) void temb_mlp_kernel(const float* t, const flo
 }
 
 // Row-parallel dense layer over a batch of <= 32 utterances, the time-embedding path (ncsnpp.py:256-275,
-// layerspp.py:264-265):  out[b][r] = act_out(bias[r] + sum_d W[r][d] * in_b[d]),  D <= 512, where in_b is
+// layerspp.py:264-265):  out[b][r] = act_out(bias[r] + sum_d W[r][d] * in_b[d]),  D <= 512, D % 4 == 0, where in_b is
 //   IN 0: x[b] as given, IN 1: silu(x[b]) (the Dense_0 input), IN 2: the Gaussian-Fourier projection of t[b]
 //   ([sin, cos](2 pi log(t) W_gfp), nf = D / 2 frequencies); act_out = silu for OUT 1.
-// Block = 4 waves; the [32][512] input table is staged in LDS.  A wave requests its kDenseRowsPerWave weight
-// rows up front as coalesced 2 KB lines (lane = 8 consecutive d), forms the 2 x 32 per-lane partial dot
-// products of each row pair against every utterance's LDS row and reduces them with one 64-wide bfly_sum:
-// lane l ends with row l / 32, utterance l % 32.  Every launch reads each weight row once, spread over the
-// chip.  (The previous forms -- an MLP block per utterance streaming all 1.5 MB of W1, W2 through one CU, and
-// a lane-per-row Dense_0 table -- ran ~60 and ~68 us per launch, profiles/r05a_c2_dispatch_shapes.jsonl.)
-constexpr int kDenseRowsPerWave = 8;
+// Block = 4 waves; the [32][SR] input table is staged in LDS.  A wave owns 16 weight rows and computes all 32
+// utterances as two 16 x 16 tiles on the exact-fp32 MFMA (v_mfma_f32_16x16x4_f32): per 16 inputs a lane loads 4
+// consecutive weights of its row and 4 table entries of its utterance, and the 4 MFMAs take component q, so the
+// tile's K index g = lane / 16 stands for input 4 g + q on both operands.  (Wave-wide shuffle reductions ran
+// 20-27 us per launch on a chain of ~500 waits, a block per utterance ~44 us, a lane-per-row table ~68 us;
+// profiles/r05a..r05l dispatch shapes.)
+constexpr int kDenseSR = 516;  // LDS row stride (floats): 16 utterance rows x 16 B reads hit distinct banks
 template <int IN, int OUT>
 __global__ __launch_bounds__(256) void temb_dense_kernel(const float* x, const float* t, const float* Wg,
                                                          const float* W, const float* bias, float* out, int B, int R,
                                                          int D) {
-  extern __shared__ __attribute__((aligned(16))) float st[];  // [32][512] input rows, zero beyond (B, D)
+  extern __shared__ __attribute__((aligned(16))) float st[];  // [32][kDenseSR] input rows, zero beyond (B, D)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  // staging: all of a thread's loads issued before any is used (a load-use chain per element held every launch
-  // of this kernel near 30-45 us whatever its size)
+  // staging: all of a thread's loads issued before any is used
   if constexpr (IN == 2) {
     const int nf = D >> 1;
-    for (int i = tid; i < 32 * 512; i += 256) {
-      const int bb = i >> 9, d = i & 511;
-      if (bb >= B || d >= 2 * nf) st[i] = 0.f;
+    for (int i = tid; i < 32 * 128; i += 256) {
+      const int bb = i >> 7, d = (i & 127) * 4;
+      if (bb >= B || d >= D) *(f32x4*)(st + bb * kDenseSR + d) = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll 4
     for (int i = tid; i < B * nf; i += 256) {
       const int bb = i / nf, k = i - bb * nf;
       float sn, cs;
       sincosf(logf(t[bb]) * Wg[k] * kTwoPi, &sn, &cs);
-      st[bb * 512 + k] = sn;
-      st[bb * 512 + nf + k] = cs;
+      st[bb * kDenseSR + k] = sn;
+      st[bb * kDenseSR + nf + k] = cs;
     }
   } else {
     constexpr int NQ = 32 * 512 / 4 / 256;  // f32x4 pieces per thread
@@ -124,38 +123,47 @@ __global__ __launch_bounds__(256) void temb_dense_kernel(const float* x, const f
           for (int e = 0; e < 4; ++e) a[e] = silu_exact(a[e]);
         }
       }
-      *(f32x4*)(st + bb * 512 + d) = a;
+      *(f32x4*)(st + bb * kDenseSR + d) = a;
     }
   }
   __syncthreads();
-  const int d0 = 8 * lane;
-  const bool dok = d0 < D;  // D % 4 == 0 and D <= 512: a lane's 8 inputs are all valid or (second half) zero
-  const bool dok2 = d0 + 4 < D;
-  const int rw0 = (blockIdx.x * 4 + wid) * kDenseRowsPerWave;
-  f32x4 wall[kDenseRowsPerWave][2];
+  const int r0 = (blockIdx.x * 4 + wid) * 16;
+  if (r0 >= R) return;  // wave-uniform, no barrier follows
+  const int n = lane & 15, g = lane >> 4;
+  const float* wrow = W + (size_t)min(r0 + n, R - 1) * D;
+  const float* s0 = st + n * kDenseSR + 4 * g;
+  const float* s1 = st + (16 + n) * kDenseSR + 4 * g;
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  constexpr int KB = 8;  // 16-input steps whose weight loads are in flight together
+  for (int k0 = 0; k0 < D; k0 += 16 * KB) {
+    f32x4 bw[KB];
 #pragma unroll
-  for (int q = 0; q < kDenseRowsPerWave; ++q) {
-    const int r = min(rw0 + q, R - 1);
-    const float* wp = W + (size_t)r * D + d0;
-    wall[q][0] = dok ? *(const f32x4*)wp : f32x4{0.f, 0.f, 0.f, 0.f};
-    wall[q][1] = dok2 ? *(const f32x4*)(wp + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int rp = 0; rp < kDenseRowsPerWave; rp += 2) {
-    const int r0 = rw0 + rp;
-    if (r0 >= R) break;  // wave-uniform
-    float pp[64];
-#pragma unroll
-    for (int bb = 0; bb < 32; ++bb) {
-      const f32x4 s0 = *(const f32x4*)(st + bb * 512 + d0), s1 = *(const f32x4*)(st + bb * 512 + d0 + 4);
-      pp[bb] = dot4(wall[rp][0], s0) + dot4(wall[rp][1], s1);
-      pp[32 + bb] = dot4(wall[rp + 1][0], s0) + dot4(wall[rp + 1][1], s1);
+    for (int u = 0; u < KB; ++u) {
+      const int k = k0 + 16 * u + 4 * g;
+      bw[u] = k < D ? *(const f32x4*)(wrow + k) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    const float v = bfly_sum<64>(pp, lane);
-    const int r = r0 + (lane >> 5), bb = lane & 31;
-    if (r < R && bb < B) {
-      const float y = v + bias[r];
-      out[(size_t)bb * R + r] = OUT == 1 ? silu_exact(y) : y;
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+      const int k = k0 + 16 * u;  // (table columns past D are zero, rows stay inside the 512-column table)
+      const f32x4 a0 = k < D ? *(const f32x4*)(s0 + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 a1 = k < D ? *(const f32x4*)(s1 + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[q], bw[u][q], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[q], bw[u][q], acc1, 0, 0, 0);
+      }
+    }
+  }
+  // acc: D[utterance 4 g + j (+16)][row r0 + n]
+  const int r = r0 + n;
+  if (r < R) {
+    const float bi = bias[r];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int b0 = 4 * g + j, b1 = 16 + 4 * g + j;
+      const float y0 = acc0[j] + bi, y1 = acc1[j] + bi;
+      if (b0 < B) out[(size_t)b0 * R + r] = OUT == 1 ? silu_exact(y0) : y0;
+      if (b1 < B) out[(size_t)b1 * R + r] = OUT == 1 ? silu_exact(y1) : y1;
     }
   }
 }
@@ -164,13 +172,13 @@ template <int IN, int OUT>
 int launch_dense(const float* x, const float* t, const float* Wg, const float* W, const float* bias, float* out, int B,
                  int R, int D, hipStream_t s) {
   static const hipError_t attr = hipFuncSetAttribute((const void*)temb_dense_kernel<IN, OUT>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 32 * 512 * 4);
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 32 * kDenseSR * 4);
   SNRSE_RET(attr);
-  const int rows_per_block = 4 * kDenseRowsPerWave;
+  const int rows_per_block = 4 * 16;
   for (int b0 = 0; b0 < B; b0 += 32) {  // the LDS table holds 32 utterances
     const int nb = std::min(32, B - b0);
     hipLaunchKernelGGL((temb_dense_kernel<IN, OUT>), dim3((R + rows_per_block - 1) / rows_per_block), dim3(256),
-                       sizeof(float) * 32 * 512, s, x ? x + (size_t)b0 * D : nullptr, t ? t + b0 : nullptr, Wg, W,
+                       sizeof(float) * 32 * kDenseSR, s, x ? x + (size_t)b0 * D : nullptr, t ? t + b0 : nullptr, Wg, W,
                        bias, out + (size_t)b0 * R, nb, R, D);
     SNRSE_LAUNCH_CHECK();
   }
