@@ -183,7 +183,9 @@ int snrse_set_option(const char* name, int value);
 int snrse_get_option(const char* name, int* value);
 
 /* AttnBlockpp attention core (layerspp.py:84-88): qkv [B][L][3C] -> out [B][L][C],
- * softmax(q k^T / sqrt(C)) v, flash-style on MFMA.  C must be 256. */
+ * softmax(q k^T / sqrt(C)) v, flash-style on MFMA.  C must be 256.  dtype SNRSE_BF16, SNRSE_F32 (exact fp32
+ * MFMAs) or SNRSE_F32X3 (fp32 in / out, q, k, v and the probabilities split into bf16 hi + lo, hi.hi + hi.lo + lo.hi
+ * products: the fp32x3 parity mode). */
 int snrse_attention(const void* qkv, void* out, int B, int L, int C, int dtype, hipStream_t stream);
 
 /* Time embedding (ncsnpp.py:256-275): temb[b] = W2 silu(W1 [sin, cos](2 pi log t W_gfp) + b1) + b2. */

@@ -2266,6 +2266,11 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
         cx.last_ksplit = 1;
         return launch_head_x3(q, stream);
       }
+      if (q.Cout <= 16 && cx.conv_variant != 1 && cx.head_small && head_small_ok(q)) {  // small-image heads
+        cx.last_kernel = 14;
+        cx.last_ksplit = 1;
+        return launch_head_small(q, stream, true);
+      }
       if (q.gn_scale) return SNRSE_EINVAL;  // the fused GroupNorm exists on the halo forms only
       cx.last_kernel = 3;
       if (q.Cout <= 16) return launch_x3<128, 16, 4, 1>(q, stream, cx);  // the pyramid heads (16 padded rows)

@@ -107,7 +107,7 @@ SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
 int launch_head(const ConvParams& p, hipStream_t s);
 int launch_head_x3(const ConvParams& p, hipStream_t s);
 bool head_ok(const ConvParams& p);
-int launch_head_small(const ConvParams& p, hipStream_t s);
+int launch_head_small(const ConvParams& p, hipStream_t s, bool split = false);
 bool head_small_ok(const ConvParams& p);
 
 // Epilogue flags as a compile-time mask (EF >= 0: the halo GEMMs' common configurations, no per-pass

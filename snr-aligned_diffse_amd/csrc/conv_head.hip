@@ -350,7 +350,9 @@ __global__ __launch_bounds__(256) void conv_head_x3_kernel(ConvParams p) {
 // co l % 4): the 32 results are one contiguous 128-B f32 store.  Cout == 4, C1 == 0, C0 % 256 == 0.
 constexpr int KS_PX = 8;
 
-template <int GNM>
+// SPLIT (the fp32x3 mode): fp32 input (16-B loads of 4 channels) and weights pre-split per 32-element K-tile into
+// 32 hi then 32 lo bf16 (ops.split_weight); the lane's weights are hi + lo in fp32, so the head is exact fp32 FMAs.
+template <int GNM, bool SPLIT>
 __global__ __launch_bounds__(256) void conv_head_small_kernel(ConvParams p) {
   const int lane = threadIdx.x & 63;
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -361,7 +363,6 @@ __global__ __launch_bounds__(256) void conv_head_small_kernel(ConvParams p) {
   const int y = t % p.H, b = t / p.H;
   const int x0 = xw * KS_PX;
   const int C = p.C0, K1 = 9 * C;
-  const bf16_t* src = (const bf16_t*)p.src0;
   const bf16_t* wg = (const bf16_t*)p.wgt;
   float acc[KS_PX][4];
 #pragma unroll
@@ -370,11 +371,29 @@ __global__ __launch_bounds__(256) void conv_head_small_kernel(ConvParams p) {
     for (int co = 0; co < 4; ++co) acc[i][co] = 0.f;
   for (int c0 = 0; c0 < C; c0 += 256) {
     const int c = c0 + 4 * lane;
-    uint2 wq[9][4];
+    f32x4 wq[9][4];
 #pragma unroll
     for (int tp = 0; tp < 9; ++tp)
 #pragma unroll
-      for (int co = 0; co < 4; ++co) wq[tp][co] = *(const uint2*)(wg + (size_t)co * K1 + tp * C + c);
+      for (int co = 0; co < 4; ++co) {
+        const int k = tp * C + c;
+        uint2 h;
+        f32x4 w;
+        if constexpr (SPLIT) {
+          const bf16_t* wp = wg + (size_t)co * 2 * K1 + (k >> 5) * 64 + (k & 31);
+          h = *(const uint2*)wp;
+          const uint2 l = *(const uint2*)(wp + 32);
+          w = f32x4{__uint_as_float(h.x << 16) + __uint_as_float(l.x << 16),
+                    __uint_as_float(h.x & 0xffff0000u) + __uint_as_float(l.x & 0xffff0000u),
+                    __uint_as_float(h.y << 16) + __uint_as_float(l.y << 16),
+                    __uint_as_float(h.y & 0xffff0000u) + __uint_as_float(l.y & 0xffff0000u)};
+        } else {
+          h = *(const uint2*)(wg + (size_t)co * K1 + k);
+          w = f32x4{__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xffff0000u), __uint_as_float(h.y << 16),
+                    __uint_as_float(h.y & 0xffff0000u)};
+        }
+        wq[tp][co] = w;
+      }
     f32x4 gs = {1.f, 1.f, 1.f, 1.f}, gh = {0.f, 0.f, 0.f, 0.f};
     if constexpr (GNM > 0) {
       gs = *(const f32x4*)(p.gn_scale + (size_t)b * C + c);
@@ -388,14 +407,21 @@ __global__ __launch_bounds__(256) void conv_head_small_kernel(ConvParams p) {
       for (int j = 0; j < KS_PX + 2; ++j) {
         const int xx = x0 - 1 + j;
         if (xx < 0 || xx >= p.W) continue;  // wave-uniform
-        const uint2 raw = *(const uint2*)(src + (((size_t)b * p.H + yy) * p.W + xx) * C + c);
-        float v[4] = {__uint_as_float(raw.x << 16), __uint_as_float(raw.x & 0xffff0000u),
-                      __uint_as_float(raw.y << 16), __uint_as_float(raw.y & 0xffff0000u)};
+        const size_t pix = ((size_t)b * p.H + yy) * p.W + xx;
+        float v[4];
+        if constexpr (SPLIT) {
+          const f32x4 r = *(const f32x4*)((const float*)p.src0 + pix * C + c);
+          v[0] = r[0]; v[1] = r[1]; v[2] = r[2]; v[3] = r[3];
+        } else {
+          const uint2 raw = *(const uint2*)((const bf16_t*)p.src0 + pix * C + c);
+          v[0] = __uint_as_float(raw.x << 16); v[1] = __uint_as_float(raw.x & 0xffff0000u);
+          v[2] = __uint_as_float(raw.y << 16); v[3] = __uint_as_float(raw.y & 0xffff0000u);
+        }
         if constexpr (GNM > 0) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const float a = fmaf(v[e], gs[e], gh[e]);
-            v[e] = GNM == 2 ? silu(a) : a;
+            v[e] = GNM == 2 ? (SPLIT ? silu_exact(a) : silu(a)) : a;
           }
         }
 #pragma unroll
@@ -405,12 +431,12 @@ __global__ __launch_bounds__(256) void conv_head_small_kernel(ConvParams p) {
           const int tp = (dy + 1) * 3 + dx + 1;
 #pragma unroll
           for (int co = 0; co < 4; ++co) {
-            const uint2 w = wq[tp][co];
+            const f32x4 w = wq[tp][co];
             float a = acc[i][co];
-            a = fmaf(v[0], __uint_as_float(w.x << 16), a);
-            a = fmaf(v[1], __uint_as_float(w.x & 0xffff0000u), a);
-            a = fmaf(v[2], __uint_as_float(w.y << 16), a);
-            a = fmaf(v[3], __uint_as_float(w.y & 0xffff0000u), a);
+            a = fmaf(v[0], w[0], a);
+            a = fmaf(v[1], w[1], a);
+            a = fmaf(v[2], w[2], a);
+            a = fmaf(v[3], w[3], a);
             acc[i][co] = a;
           }
         }
@@ -438,13 +464,22 @@ bool head_small_ok(const ConvParams& p) {
   return (long long)p.B * p.H * ((p.W + KS_PX - 1) / KS_PX) < 0x7fffffffLL;
 }
 
-int launch_head_small(const ConvParams& p, hipStream_t s) {
+// split: the fp32x3 form (fp32 input, split weights)
+int launch_head_small(const ConvParams& p, hipStream_t s, bool split) {
   if (!head_small_ok(p)) return SNRSE_EINVAL;
   const long long waves = (long long)p.B * p.H * ((p.W + KS_PX - 1) / KS_PX);
   const unsigned blocks = (unsigned)((waves + 3) / 4);
-  if (!p.gn_scale) hipLaunchKernelGGL(conv_head_small_kernel<0>, dim3(blocks), dim3(256), 0, s, p);
-  else if (!p.gn_act) hipLaunchKernelGGL(conv_head_small_kernel<1>, dim3(blocks), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(conv_head_small_kernel<2>, dim3(blocks), dim3(256), 0, s, p);
+#define SNRSE_HS(G_, S_) hipLaunchKernelGGL((conv_head_small_kernel<G_, S_>), dim3(blocks), dim3(256), 0, s, p)
+  if (split) {
+    if (!p.gn_scale) SNRSE_HS(0, true);
+    else if (!p.gn_act) SNRSE_HS(1, true);
+    else SNRSE_HS(2, true);
+  } else {
+    if (!p.gn_scale) SNRSE_HS(0, false);
+    else if (!p.gn_act) SNRSE_HS(1, false);
+    else SNRSE_HS(2, false);
+  }
+#undef SNRSE_HS
   return (int)hipGetLastError();
 }
 

@@ -117,8 +117,8 @@ class NCSNppHIP:
 
     def __init__(self, sd: dict, dtype=torch.bfloat16, device="cuda", gemm="exact", **cfg):
         """gemm (fp32 only): "exact" = v_mfma_f32_16x16x4_f32 GEMMs; "x3" = the split-bf16 GEMM
-        (ops.split_weight, three bf16 products per K-tile) for the ResBlock and input convs, exact fp32
-        for the attention projections and the pyramid heads."""
+        (ops.split_weight, three bf16 products per K-tile) for every conv: the ResBlock, input and pyramid-head
+        convs and (round 5) the attention projections NIN_0..3 and the attention core (split q, k, v, p)."""
         if not torch.cuda.is_available():
             raise RuntimeError("snrse: NCSNppHIP needs a HIP device (no CPU fallback)")
         if gemm not in ("exact", "x3") or (gemm == "x3" and dtype != torch.float32):
@@ -195,6 +195,9 @@ class NCSNppHIP:
                             e[k] = ops.split_weight(e[k])
                 elif m.kind == "conv3x3" and "w" in e:
                     e["w"] = ops.split_weight(e["w"])
+                elif m.kind == "attn":  # the 1x1 QKV / NIN_3 projections (exact fp32 GEMMs before round 5)
+                    e["wqkv"] = ops.split_weight(e["wqkv"])
+                    e["w3"] = ops.split_weight(e["w3"])
 
     # ------------------------------------------------------------------ blocks
     # Every activation travels with its per-channel GroupNorm statistics, produced by the
@@ -249,7 +252,7 @@ class NCSNppHIP:
         t, s = x
         a = ops.gn_apply(t, None, s, e["gn_g"], e["gn_b"], act=False)
         qkv, _ = self._conv(a, e["wqkv"], 1, 3 * m.cout, bias=e["bqkv"], want_stats=False)
-        o = ops.attention(qkv, m.cout)
+        o = ops.attention(qkv, m.cout, split=self.gemm == "x3")
         return self._conv(o, e["w3"], 1, m.cout, bias=e["b3"], res=t, out_scale=INV_SQRT2)
 
     def _pyramid_head(self, gn_m, conv_m, h, pyr_up):

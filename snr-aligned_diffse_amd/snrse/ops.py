@@ -270,8 +270,8 @@ def x3h_ok(x, ksize, cout):
 def head_ok(x, split=False):
     """True when a 3x3 conv of x with Cout = 4 and f32 output (the pyramid heads) takes a head kernel that
     accepts a fused GroupNorm (gn=): the halo-staged head (bf16 x, or f32 x with split weights: split=True, the
-    fp32x3 mode's conv_head_x3_kernel; H % 8 == 0, W % 32 == 0), or for bf16 x with C % 256 == 0 the
-    wave-per-8-pixels head of the other image sizes (option head_small, snrse_conv2d)."""
+    fp32x3 mode's conv_head_x3_kernel; H % 8 == 0, W % 32 == 0), or with C % 256 == 0 the wave-per-8-pixels
+    head of the other image sizes (bf16, or the fp32x3 form; option head_small, snrse_conv2d)."""
     B, H, W, C = x.shape
     if _opt(x, "conv_variant") == 1:
         return False
@@ -279,7 +279,7 @@ def head_ok(x, split=False):
     # channels: the C-ABI's K-tile (64 bf16 / 32 f32 channels, snrse_conv2d)
     if dt_ok and H % 8 == 0 and W % 32 == 0 and C % (64 if x.dtype == torch.bfloat16 else 32) == 0:
         return True
-    return x.dtype == torch.bfloat16 and C % 256 == 0 and _opt(x, "head_small") != 0
+    return dt_ok and C % 256 == 0 and _opt(x, "head_small") != 0
 
 
 def gn_scale_shift(sums0, gamma, beta, HW, sums1=None, groups=None, eps=1e-6):
@@ -468,11 +468,16 @@ def fir(x, mode):
     return gn_apply(x, act=False, mode=mode)
 
 
-def attention(qkv, C=256):
+def attention(qkv, C=256, split=False):
+    """softmax(q k^T / sqrt(C)) v (layerspp.py:84-88) of qkv [B, L(, W), 3C]; split=True (fp32 only): the fp32x3
+    mode's split-bf16 products (snrse_attention with SNRSE_F32X3) instead of exact fp32 MFMAs."""
     _dev(qkv)
     B, L = qkv.shape[0], qkv.shape[1] * (qkv.shape[2] if qkv.dim() == 4 else 1)
     out = torch.empty(*qkv.shape[:-1], C, device=qkv.device, dtype=qkv.dtype)
-    _lib.call("snrse_attention", qkv.data_ptr(), out.data_ptr(), B, L, C, code(qkv.dtype), _stream())
+    if split and qkv.dtype != torch.float32:
+        raise TypeError("snrse: split attention takes fp32 q, k, v")
+    _lib.call("snrse_attention", qkv.data_ptr(), out.data_ptr(), B, L, C, _lib.F32X3 if split else code(qkv.dtype),
+              _stream())
     return out
 
 

@@ -243,11 +243,13 @@ def test_upfirdn2d_half_double(gpu, dtype, atol):
         np.testing.assert_allclose(up.cpu().numpy(), g["up"], atol=1e-5)
 
 
-@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("dt", ["f32", "bf16", "x3"])
 @pytest.mark.parametrize("L", [128, 37, 512, 100])
 def test_attention_core(gpu, dt, L):
+    """Attention core (layerspp.py:84-88) vs float64: exact fp32, bf16, and the fp32x3 mode's split-bf16 products
+    (x3: <= 3e-5 relative; ragged L masks the last key block)."""
     from snrse import ops
-    dtype, tol = DT[dt]
+    dtype, tol = DT["f32" if dt == "x3" else dt]
     B, C = 2, 256
     qkv = torch.from_numpy(fnormal("t.at.qkv", (B, L, 3 * C)))
     if dt == "bf16":
@@ -255,8 +257,8 @@ def test_attention_core(gpu, dt, L):
     q, k, v = qkv.double().split(C, dim=2)
     p = torch.softmax(q @ k.transpose(1, 2) / 16.0, dim=-1)
     ref = p @ v
-    out = ops.attention(qkv.to(gpu, dtype).contiguous(), C)
-    assert rel(out.float(), ref) < (tol if dt == "f32" else 2e-2)
+    out = ops.attention(qkv.to(gpu, dtype).contiguous(), C, split=dt == "x3")
+    assert rel(out.float(), ref) < {"f32": tol, "bf16": 2e-2, "x3": 3e-5}[dt]
 
 
 def test_attn_block_golden(gpu):
@@ -712,17 +714,23 @@ def test_conv_head_fused_groupnorm(gpu, shape):
     assert rel(nchw(out), ref) < 1e-2
 
 
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("shape,act,small", [((32, 256, 4, 8), True, 1), ((32, 256, 8, 16), True, 1),
                                              ((3, 512, 5, 11), True, 1), ((2, 256, 7, 3), False, 1),
                                              ((4, 256, 16, 32), True, 2), ((2, 256, 8, 16), None, 1)])
-def test_conv_head_small(gpu, shape, act, small):
+def test_conv_head_small(gpu, shape, act, small, split):
     """Pyramid heads of the small levels (ncsnpp.py:348-366: the 8 x 16 and 4 x 8 levels of C2, which the tiled
     head cannot take) through the wave-per-8-pixels head with the GroupNorm(+SiLU) fused (act None: no norm);
-    ragged widths and heights, 2 channel passes, and option head_small 2 on a tiled-head shape."""
+    ragged widths and heights, 2 channel passes, and option head_small 2 on a tiled-head shape.  split: the
+    fp32x3 form (fp32 input, ops.split_weight weights; exact fp32 FMAs, 3e-5)."""
     from snrse import ops
+    if split and small == 2:
+        pytest.skip("head_small 2 selects between the bf16 heads only")
     B, C, H, W = shape
-    x = (torch.from_numpy(fnormal("t.hs.x", (B, C, H, W))) * 1.5 + 0.2).bfloat16().float()
-    w = (torch.from_numpy(fnormal("t.hs.w", (4, C, 3, 3))) / 48).bfloat16().float()
+    x = (torch.from_numpy(fnormal("t.hs.x", (B, C, H, W))) * 1.5 + 0.2)
+    w = (torch.from_numpy(fnormal("t.hs.w", (4, C, 3, 3))) / 48)
+    if not split:
+        x, w = x.bfloat16().float(), w.bfloat16().float()
     b = torch.from_numpy(fnormal("t.hs.b", (4,)))
     r = torch.from_numpy(fnormal("t.hs.r", (B, 4, H, W)))
     g = torch.from_numpy(fnormal("t.hs.g", (C,))) * 0.1 + 1
@@ -733,22 +741,23 @@ def test_conv_head_small(gpu, shape, act, small):
         a = F.group_norm(x.double(), min(C // 4, 32), g.double(), be.double(), eps=1e-6)
         a = F.silu(a) if act else a
     ref = (F.conv2d(a, w.double(), b.double(), padding=1) + r.double()) * 0.75
-    xg = nhwc(x).to(gpu, torch.bfloat16)
+    xg = nhwc(x).to(gpu, torch.float32 if split else torch.bfloat16)
     gn = None
     if act is not None:
         sums, _ = ops.gn_stats(xg)
         gn = ops.gn_scale_shift(sums, g.to(gpu), be.to(gpu), H * W)
-    wp = torch.cat([w.permute(0, 2, 3, 1).reshape(4, -1), torch.zeros(12, 9 * C)]).to(gpu, torch.bfloat16).contiguous()
+    wp = torch.cat([w.permute(0, 2, 3, 1).reshape(4, -1), torch.zeros(12, 9 * C)]).to(gpu)
+    wp = ops.split_weight(wp) if split else wp.to(torch.bfloat16).contiguous()
     ops.set_option("head_small", small)
     try:
-        assert ops.head_ok(xg)
+        assert ops.head_ok(xg, split=split)
         out = ops.conv2d(xg, wp, 3, 4, bias=b.to(gpu), res=nhwc(r).to(gpu), out_f32=True, gn=gn,
                          gn_act=bool(act), out_scale=0.75)
         assert ops.kernel_name(ops.get_option("last_kernel")) == "conv_head_small_kernel"
     finally:
         ops.set_option("head_small", 1)
     assert out.dtype == torch.float32
-    assert rel(nchw(out), ref) < 1e-3
+    assert rel(nchw(out), ref) < (3e-5 if split else 1e-3)
 
 
 @pytest.mark.parametrize("shape", [(32, 256, 4, 8), (6, 256, 2, 4), (5, 128, 4, 4), (3, 256, 3, 5)])

@@ -105,8 +105,10 @@ def test_x3_residual_and_layout_errors(gpu):
         ops.conv2d(nhwc(x).to(gpu), ops.split_weight(torch.zeros(64, 9 * C, device=gpu)), 3, 64)
 
 
-def test_x3_pyramid_head(gpu):
-    """Cout = 4 (16 padded rows) with the upsampled pyramid as an fp32 residual: the heads' split GEMM."""
+@pytest.mark.parametrize("head_small", [1, 0])
+def test_x3_pyramid_head(gpu, head_small):
+    """Cout = 4 (16 padded rows) with the upsampled pyramid as an fp32 residual at a size the tiled head cannot
+    take: the wave-per-8-pixels fp32x3 head (option head_small 1, the default) and the heads' split GEMM (0)."""
     from snrse import ops
     B, cin, H, W = 2, 256, 8, 16
     x = torch.from_numpy(fnormal("t.py.x", (B, cin, H, W)))
@@ -115,8 +117,13 @@ def test_x3_pyramid_head(gpu):
     r = torch.from_numpy(fnormal("t.py.r", (B, 4, H, W)))
     ref = F.conv2d(x.double(), w.double(), b.double(), padding=1) + r.double()
     wp = torch.cat([w.permute(0, 2, 3, 1).reshape(4, -1), torch.zeros(12, 9 * cin)]).to(gpu)
-    out = ops.conv2d(nhwc(x).to(gpu), ops.split_weight(wp), 3, 4, bias=b.to(gpu), res=nhwc(r).to(gpu), out_f32=True)
-    assert ops.get_option("last_kernel") == 3
+    ops.set_option("head_small", head_small)
+    try:
+        out = ops.conv2d(nhwc(x).to(gpu), ops.split_weight(wp), 3, 4, bias=b.to(gpu), res=nhwc(r).to(gpu),
+                         out_f32=True)
+        assert ops.get_option("last_kernel") == (14 if head_small else 3)
+    finally:
+        ops.set_option("head_small", 1)
     assert out.dtype == torch.float32
     assert rel(nchw(out), ref) < TOL
 
