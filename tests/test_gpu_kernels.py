@@ -139,6 +139,28 @@ def test_conv_small_cout_pyramid(gpu, dt):
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("HW", [(16, 32), (4, 8), (16, 64), (3, 5)])
+def test_gn_apply_small_image_single_launch(gpu, dt, HW):
+    """GroupNorm(+SiLU) apply on both sides of ops.GN_FUSED_MAX_HW (512 px): one launch that folds the slotted
+    statistics per block (the 16 x 32 .. 4 x 8 levels, ragged 3 x 5) and the gn_scale_shift + gn_act pair above
+    it, over a concatenated input, against float64 (layerspp.py:245-247, GroupNorm_0 + act)."""
+    from snrse import ops
+    dtype, tol = DT[dt]
+    B, C0, C1 = 3, 256, 256
+    H, W = HW
+    x = torch.from_numpy(fnormal("t.gs.x", (B, C0 + C1, H, W))) * 1.5 - 0.2
+    g = torch.from_numpy(fnormal("t.gs.g", (C0 + C1,))) * 0.1 + 1
+    be = torch.from_numpy(fnormal("t.gs.b", (C0 + C1,))) * 0.1
+    if dt == "bf16":
+        x = x.bfloat16().float()
+    ref = F.silu(F.group_norm(x.double(), 32, g.double(), be.double(), eps=1e-6))
+    xg = nhwc(x).to(gpu, dtype)
+    s0, s1 = xg[..., :C0].contiguous(), xg[..., C0:].contiguous()
+    out = ops.gn_apply(s0, s1, ops.gn_stats(s0, s1), g.to(gpu), be.to(gpu), act=True)
+    assert rel(nchw(out.float()), ref) < tol
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("mode", ["none", "down", "up"])
 @pytest.mark.parametrize("C", [128, 384])
 def test_gn_silu_fir(gpu, dt, mode, C):
