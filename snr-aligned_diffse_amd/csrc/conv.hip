@@ -58,7 +58,7 @@ SNRSE_DEV void block_stats_flush(const ConvParams& p, const float* red, int blk_
 
 // nvalid < 64: only the wave's first nvalid rows are output pixels (a tile cut by the image's right
 // edge, conv_x3h_kernel); the rest are skipped.
-template <typename TO, int NWM, int BN, bool DEFER = false>
+template <typename TO, int NWM, int BN, bool DEFER = false, int LA = 8>
 SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int mb, int nb, int lane, float* stage,
                             float* red, int wm, int blk_b, int blk_n0, int nvalid = 64) {
   constexpr int LDR = 68;  // padded row (floats): conflict-free C-layout writes
@@ -99,6 +99,29 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
   // atomics made a 1024-px 1x1 conv take 156 us, profiles/r05a_c2_dispatch_shapes.jsonl).
   const bool seg = p.stats && !one_b && HW % RPP == 0;
   int seg_b = -1;
+  // the image's temb row joins the bias when the tile lies in one image; the residual / Combine inputs are
+  // requested LA passes ahead of their use (LA of the 8 bf16 / 16 f32 passes; the caller sizes it to its
+  // register budget), not one round trip per pass (with vmcnt in order, each such wait also drained the
+  // earlier passes' stores)
+  if (p.temb && one_b && nok) {
+    const float* tb = p.temb + (size_t)(mb / HW) * p.temb_stride + n;
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) bias[k] += tb[k];
+  }
+  constexpr int NPASS = 64 / RPP;
+  static_assert(LA >= 1 && LA <= NPASS, "lookahead");
+  u32x4 rpre[NPASS];
+  f32x4 qpre[NPASS];
+  auto epi_issue = [&](int pass) {
+    const int row = r0 + pass * RPP;
+    const int m = mb + row;
+    if (m < p.M && nok && row < nvalid) {
+      if (p.res) rpre[pass] = *(const u32x4*)((const TO*)p.res + (size_t)m * p.res_ld + n);
+      if (p.comb_src) qpre[pass] = *(const f32x4*)(p.comb_src + (size_t)m * 4);
+    }
+  };
+#pragma unroll
+  for (int pass = 0; pass < LA; ++pass) epi_issue(pass);
   float s1[EPC], s2[EPC];
 #pragma unroll
   for (int k = 0; k < EPC; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
@@ -123,7 +146,8 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
     for (int k = 0; k < EPC; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
   };
 #pragma unroll
-  for (int pass = 0; pass < 64 / RPP; ++pass) {
+  for (int pass = 0; pass < NPASS; ++pass) {
+    if (pass + LA < NPASS) epi_issue(pass + LA);
     const int row = r0 + pass * RPP;
     const int m = mb + row;
     if (seg) {
@@ -138,13 +162,13 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
     const float* sr = stage + row * LDR + cc * EPC;
 #pragma unroll
     for (int k = 0; k < EPC; ++k) v[k] = sr[k] + bias[k];
-    if (p.temb) {
+    if (p.temb && !one_b) {
       const float* tb = p.temb + (size_t)(m / HW) * p.temb_stride + n;
 #pragma unroll
       for (int k = 0; k < EPC; ++k) v[k] += tb[k];
     }
     if (p.res) {
-      const u32x4 rv = *(const u32x4*)((const TO*)p.res + (size_t)m * p.res_ld + n);
+      const u32x4 rv = rpre[pass];
       if constexpr (sizeof(TO) == 2) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -159,7 +183,7 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
 #pragma unroll
     for (int k = 0; k < EPC; ++k) v[k] *= p.out_scale;
     if (p.comb_src) {
-      const f32x4 q = *(const f32x4*)(p.comb_src + (size_t)m * 4);
+      const f32x4 q = qpre[pass];
 #pragma unroll
       for (int k = 0; k < EPC; ++k) v[k] += q[0] * cw[k][0] + q[1] * cw[k][1] + q[2] * cw[k][2] + q[3] * cw[k][3] + cb[k];
     }
@@ -245,7 +269,7 @@ SNRSE_DEV int epi_pix(int mb, int row, int seg_skip) {
   return TW == 64 ? mb + row : mb + row + (row / TW) * seg_skip;
 }
 
-template <typename TO, int NWM, int BN, bool DEFER, int EF = EF_RT, int TW = 64>
+template <typename TO, int NWM, int BN, bool DEFER, int EF = EF_RT, int TW = 64, int LA = 8>
 SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int mb, int nb, int lane, float* stage,
                             float* red, int wm, int b, int blk_n0, int seg_skip = 0) {
   const bool f_temb = EF < 0 ? p.temb != nullptr : (EF & EF_TEMB) != 0;
@@ -269,11 +293,11 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
   float add[EPC];
 #pragma unroll
   for (int k = 0; k < EPC; ++k) add[k] = 0.f;
-  if (p.bias) {
+  if (p.bias) {  // (assigned, not added to 0: an add in the branch made the compiler wait for the load there)
 #pragma unroll
     for (int k = 0; k < EPC; k += 4) {
       const f32x4 v = *(const f32x4*)(p.bias + n + k);
-      add[k] += v[0]; add[k + 1] += v[1]; add[k + 2] += v[2]; add[k + 3] += v[3];
+      add[k] = v[0]; add[k + 1] = v[1]; add[k + 2] = v[2]; add[k + 3] = v[3];
     }
   }
   if (f_temb) {
@@ -293,31 +317,26 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
   float s1[EPC], s2[EPC];
 #pragma unroll
   for (int k = 0; k < EPC; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
-  // bf16: every pass's residual / Combine input is loaded up front, so the passes do not wait on
-  // one HBM round trip each (a wait that, vmcnt being in order, also drained the earlier stores)
+  // The residual / Combine inputs are requested LA passes ahead of their use (bf16: all 8 passes up front;
+  // f32: LA of the 16, sized by the caller), so the passes do not wait on one HBM round trip each -- a wait
+  // that, vmcnt being in order, also drained the earlier passes' stores (the fp32x3 halo GEMM's residual
+  // convs did that 16 times per tile at one workgroup per CU).
   constexpr int NPASS = 64 / RPP;
-#ifndef SNRSE_EPI_PREFETCH
-#define SNRSE_EPI_PREFETCH 1
-#endif
-  constexpr bool PRE = SNRSE_EPI_PREFETCH && sizeof(TO) == 2;
-  u32x4 rpre[PRE ? NPASS : 1];
-  f32x4 qpre[PRE ? NPASS : 1];
-  if constexpr (PRE) {
-    if (f_res) {
+  static_assert(LA >= 1 && LA <= NPASS, "lookahead");
+  u32x4 rpre[NPASS];
+  f32x4 qpre[NPASS];
+  auto epi_issue = [&](int pass) {
+    const size_t m = (size_t)epi_pix<TW>(mb, r0 + pass * RPP, seg_skip);
+    if (f_res) rpre[pass] = *(const u32x4*)((const TO*)p.res + m * p.res_ld + n);
+    if (f_comb) qpre[pass] = *(const f32x4*)(p.comb_src + m * 4);
+  };
 #pragma unroll
-      for (int pass = 0; pass < NPASS; ++pass)
-        rpre[pass] = *(const u32x4*)((const TO*)p.res + (size_t)epi_pix<TW>(mb, r0 + pass * RPP, seg_skip) * p.res_ld + n);
-    }
-    if (f_comb) {
-#pragma unroll
-      for (int pass = 0; pass < NPASS; ++pass)
-        qpre[pass] = *(const f32x4*)(p.comb_src + (size_t)epi_pix<TW>(mb, r0 + pass * RPP, seg_skip) * 4);
-    }
-  }
+  for (int pass = 0; pass < LA; ++pass) epi_issue(pass);
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int pass = 0; pass < NPASS; ++pass) {
+    if (pass + LA < NPASS) epi_issue(pass + LA);
     const int row = r0 + pass * RPP;
     const size_t m = (size_t)epi_pix<TW>(mb, row, seg_skip);
     float v[EPC];
@@ -325,9 +344,7 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
 #pragma unroll
     for (int k = 0; k < EPC; ++k) v[k] = sr[k] + add[k];
     if (f_res) {
-      u32x4 rv;
-      if constexpr (PRE) rv = rpre[pass];
-      else rv = *(const u32x4*)((const TO*)p.res + m * p.res_ld + n);
+      const u32x4 rv = rpre[pass];
       if constexpr (sizeof(TO) == 2) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -344,9 +361,7 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
       for (int k = 0; k < EPC; ++k) v[k] *= p.out_scale;
     }
     if (f_comb) {
-      f32x4 q;
-      if constexpr (PRE) q = qpre[pass];
-      else q = *(const f32x4*)(p.comb_src + m * 4);
+      const f32x4 q = qpre[pass];
 #pragma unroll
       for (int k = 0; k < EPC; ++k) v[k] += q[0] * cw[k][0] + q[1] * cw[k][1] + q[2] * cw[k][2] + q[3] * cw[k][3] + cb[k];
     }
@@ -783,7 +798,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvParams p) {
   if constexpr (TM == 64 && TN == 64) {
     // LDS-staged epilogue: 16-B output stores, one statistics atomic pair per channel per block
     const int b_lo = m0 / HW, b_hi = (min(m0 + BM, p.M) - 1) / HW;
-    epilogue_lds<float, WM, BN>(p, acc, m0 + wm * TM, n0 + wn * TN, lane, (float*)(smem + wid * (64 * 68 * 4)),
+    epilogue_lds<float, WM, BN, false, 4>(p, acc, m0 + wm * TM, n0 + wn * TN, lane, (float*)(smem + wid * (64 * 68 * 4)),
                                 (float*)(smem + WM * WN * (64 * 68 * 4)), wm, b_lo == b_hi ? b_lo : -1, n0);
   } else {
     epilogue<float, FM, FN>(p, acc, m0 + wm * TM, n0 + wn * TN, lane);
@@ -1425,7 +1440,8 @@ __global__ __launch_bounds__(512) void conv_glds_kernel(ConvParams p) {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   const int b_lo = m0 / HW, b_hi = (min(m0 + BM, p.M) - 1) / HW;
-  epilogue_lds<TO, WM, BN>(p, acc, m0 + wm * TM, n0 + wn * TN, lane, (float*)(smem + wid * (64 * 68 * 4)),
+  // (f32 output: one pass ahead, so the kernel keeps the 128 registers of two workgroups per CU)
+  epilogue_lds<TO, WM, BN, false, sizeof(TO) == 2 ? 8 : 1>(p, acc, m0 + wm * TM, n0 + wn * TN, lane, (float*)(smem + wid * (64 * 68 * 4)),
                            (float*)(smem + 8 * (64 * 68 * 4)), wm, b_lo == b_hi ? b_lo : -1, n0);
 }
 
@@ -1911,11 +1927,13 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   float* const stage = (float*)(smem + wid * (64 * 68 * 4));
   float* const red = (float*)(smem + 4 * (64 * 68 * 4));
   const int mrow = (bb * p.H + h0 + wid * RW) * p.W + w0;
-  epilogue_img<TO, 4, 128, true, EF, TW>(p, acc[0], mrow, n0, lane, stage, red, wid, bb, n0, p.W - TW);
+  // (f32 output, the exact mode: residuals two passes ahead -- acc[1] is still live here, 256 registers)
+  constexpr int ELA = sizeof(TO) == 2 ? 8 : 2;
+  epilogue_img<TO, 4, 128, true, EF, TW, ELA>(p, acc[0], mrow, n0, lane, stage, red, wid, bb, n0, p.W - TW);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
   SNRSE_STAMP(26);
-  epilogue_img<TO, 4, 128, true, EF, TW>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0, p.W - TW);
+  epilogue_img<TO, 4, 128, true, EF, TW, ELA>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0, p.W - TW);
   SNRSE_STAMP(27);
   if (EF < 0 ? p.stats != nullptr : (EF & EF_STATS) != 0) block_stats_flush<4, 128>(p, red, bb, n0);
 #ifdef SNRSE_STAMPS
