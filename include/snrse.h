@@ -170,13 +170,15 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  *   main input has an even number of 32-channel chunks (else 1), 1 one tap per phase with the next chunk's halo stored
  *   one piece per tap, 0 the same stored in one go;
  * "head_small" bf16 pyramid heads (Cout 4, C % 256 == 0): 1 (default) the wave-per-8-pixels head (GroupNorm fused)
- *   where the tiled head cannot take the image (H % 8 or W % 32 != 0), 2 also for up to 16384 output pixels, 0 never. */
+ *   where the tiled head cannot take the image (H % 8 or W % 32 != 0), 2 also for up to 16384 output pixels, 0 never;
+ * "head_part" tiled bf16 pyramid head with Cout 4: 1 (default) the halo's 36 tap partials as one 1x1 GEMM then their
+ *   shifted sum (last_kernel 15), 0 nine tap GEMMs over the halo (last_kernel 10). */
 int snrse_set_option(const char* name, int value);
 
 /* Read back a switch (any name above) or: "halo_kernel" = generation of the halo conv kernel the current
  * setting dispatches a 3x3 conv to (5), "last_kernel" = generation of the most recent snrse_conv2d launch (1 v1, 2 v2,
  * 3 / 4 split-bf16 register-staged / halo, 5 halo, 10 pyramid head, 11 split-bf16 pyramid head, 14 small-image
- * pyramid head),
+ * pyramid head, 15 tap-partials pyramid head),
  * "last_ksplit" = K splits of the most recent v2 launch, "last_epi_nt" /
  * "last_chunks" = store flavour / image-range launches of the most recent halo conv, "last_tw" = its tile
  * width (32 / 64). */

@@ -135,6 +135,8 @@ struct snrse_ctx {
                                // chunk's halo stored one piece per tap, 0 the same stored in one go
   int head_small = 1;          // pyramid heads (Cout 4, bf16): 1 the wave-per-8-pixels kernel where the tiled head cannot
                                // take the image (H % 8 or W % 32), 2 also for <= 16384 output pixels, 0 never
+  int head_part = 1;           // tiled pyramid head, Cout 4 (bf16): 1 the halo's 36 tap partials as a 1x1 GEMM + shifted
+                               // sum (conv_head_part_kernel), 0 nine tap GEMMs over the halo (conv_head_kernel)
   int ic_lds = 3;              // bf16 input conv: 1 the workgroup's input rows staged in LDS (W <= 1024), 2 the same
                                // with the channels split over wave pairs (4 waves / SIMD), 3 the output staged
                                // through LDS for 1-KB contiguous stores, 0 streaming loads

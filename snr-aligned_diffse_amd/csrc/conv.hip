@@ -2185,8 +2185,9 @@ int dispatch_conv(const ConvParams& p, hipStream_t s, snrse_ctx& cx) {
     // wave-per-8-pixels head
     const bool small = cx.head_small == 2 && (long long)p.B * p.H * p.W <= 16384;
     if (cx.conv_variant != 1 && head_ok(p) && !small) {
-      cx.last_kernel = 10;
-      return launch_head(p, s);
+      const bool part = cx.head_part != 0 && p.Cout == 4;
+      cx.last_kernel = part ? 15 : 10;
+      return launch_head(p, s, part);
     }
     if (cx.conv_variant != 1 && cx.head_small && head_small_ok(p)) {
       cx.last_kernel = 14;

@@ -104,7 +104,7 @@ SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
 }
 
 // Pyramid heads (conv_head.hip): 3x3, Cout <= 16, f32 output, optional fused GroupNorm+SiLU.
-int launch_head(const ConvParams& p, hipStream_t s);
+int launch_head(const ConvParams& p, hipStream_t s, bool part = false);
 int launch_head_x3(const ConvParams& p, hipStream_t s);
 bool head_ok(const ConvParams& p);
 int launch_head_small(const ConvParams& p, hipStream_t s, bool split = false);

@@ -186,6 +186,195 @@ __global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvPar
     }
   }
 }
+// Round 5, Cout = 4: the 3 x 3 head as a 1 x 1 GEMM over the halo.  conv_head_kernel reads the halo once per
+// tap (9 x 4 pixel fragments + a weight fragment per wave and chunk: ~184 KB of LDS reads per workgroup and
+// chunk for 4 useful output channels); here every halo pixel's 36 tap partials  P[px][4 tap + co] =
+// sum_ci x[px][ci] w[co][tap][ci]  accumulate over the chunks in registers (A = halo pixels, read once per
+// chunk; B = the chunk's 36 (+ 12 zero) weight columns), and only after the last chunk does each output
+// pixel sum its 9 shifted partials,  y[px][co] = sum_tap P[px + off(tap)][4 tap + co],  staged through LDS
+// one 16-column block at a time.  LDS reads per workgroup and chunk: ~36 KB.
+constexpr int KP_PB = (KH_HROWS + 15) / 16;     // 16-pixel blocks covering the halo (22: 352 rows)
+constexpr int KP_NB = (KP_PB + 3) / 4;          // per wave (6)
+constexpr int KP_PS = 20;                       // partials row stride (floats): conflict-free column writes
+constexpr int KP_STAGE = KP_PB * 16 * KP_PS * 4;  // 28160 B: the halo (22528 B) and, at the end, a partials block
+constexpr int KP_LDS = KP_STAGE + 3 * 1024 + 2 * KH_MAXC * 4;
+
+SNRSE_DEV int kp_opaque(int v) {  // a copy the compiler cannot see through: values derived from it are recomputed
+  int r;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+// the halo pixel offsets are recomputed per chunk from an opaque copy of the thread index (a few VALU ops) instead
+// of living in six registers across the loop: at three workgroups per CU (<= 168 registers) the compiler spilled
+// one, and the reload's vmcnt(0) waited on every halo load in flight
+#define KP_LOAD_H(C_, HV)                                                                                      \
+  do {                                                                                                         \
+    const bool in_ = (C_) < nc;                                                                                \
+    const int ch_ = in_ ? (C_) * 32 : 0;                                                                       \
+    const bool u1_ = ch_ >= p.C0;                                                                              \
+    const __amdgpu_buffer_rsrc_t r_ = u1_ ? make_rsrc(p.src1, p.bytes1) : make_rsrc(p.src0, p.bytes0);         \
+    const int cs_ = u1_ ? p.C1 : p.C0, cc_ = (u1_ ? ch_ - p.C0 : ch_) + hcol * 8;                              \
+    const int tq_ = kp_opaque(tid);                                                                            \
+    _Pragma("unroll") for (int j = 0; j < KH_HJ; ++j) {                                                        \
+      const int hr_ = (tq_ >> 2) + 64 * j;                                                                     \
+      const int hy_ = hr_ / KH_HC, hx_ = hr_ - hy_ * KH_HC;                                                    \
+      const int pix_ = (b * p.H + h0 + hy_ - 1) * p.W + w0 + hx_ - 1;                                          \
+      const int voff_ = (hok[j] && in_) ? (pix_ * cs_ + cc_) * 2 : (int)0x80000000;                            \
+      HV[j] = __builtin_amdgcn_raw_buffer_load_b128(r_, voff_, 0, 0);                                          \
+    }                                                                                                          \
+  } while (0)
+#define KP_LOAD_W(C_)                                                                                          \
+  do {                                                                                                         \
+    const bool in_ = (C_) < nc;                                                                                \
+    const int col_ = tid >> 2, tap_ = col_ >> 2, co_ = col_ & 3; /* column 4 tap + co, 16-B chunk tid & 3 */    \
+    const int voff_ = (in_ && col_ < 36 && co_ < p.Cout)                                                       \
+                          ? ((co_ * K1 + tap_ * Cin + (C_) * 32 + (tid & 3) * 8) * 2)                          \
+                          : (int)0x80000000;                                                                   \
+    wv = __builtin_amdgcn_raw_buffer_load_b128(rw, voff_, 0, 0);                                               \
+  } while (0)
+
+#ifndef SNRSE_HEADP_MINB
+#define SNRSE_HEADP_MINB 3  // three workgroups per CU: <= 168 VGPR + AGPR (the 72 partials accumulators are AGPRs)
+#endif
+template <int GNM>
+__global__ __launch_bounds__(256, SNRSE_HEADP_MINB) void conv_head_part_kernel(ConvParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[KP_LDS];
+  char* const halo = smem;
+  char* const wsl = smem + KP_STAGE;
+  float* const gtab = (float*)(smem + KP_STAGE + 3 * 1024);  // [2][Cin] scale, shift (prescaled for GNM 2)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntw = p.W / KH_TW, nth = p.H / KH_TH;
+  int t = blockIdx.x;
+  const int w0 = (t % ntw) * KH_TW;
+  t /= ntw;
+  const int h0 = (t % nth) * KH_TH;
+  const int b = t / nth;
+  const int Cin = p.C0 + p.C1;
+  const int nc = Cin >> 5;
+  const int K1 = 9 * Cin;
+  const int hcol = tid & 3;
+  constexpr bool gn = GNM > 0;
+  const int lrow = lane & 15, lg = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rw = make_rsrc(p.wgt, p.wbytes);
+
+  bool hok[KH_HJ];
+#pragma unroll
+  for (int j = 0; j < KH_HJ; ++j) {
+    const int hr = (tid >> 2) + 64 * j;
+    const int hy = hr / KH_HC, hx = hr - hy * KH_HC;
+    const int ih = h0 + hy - 1, iw = w0 + hx - 1;
+    hok[j] = hr < KH_HROWS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
+  }
+  u32x4 hv[KH_HJ], hw[KH_HJ], wv;
+  // acc[k][cb]: P[px = 16 (wid + 4 k) + 4 lg + e][col = 16 cb + lrow]
+  f32x4 acc[KP_NB][3];
+#pragma unroll
+  for (int k = 0; k < KP_NB; ++k)
+#pragma unroll
+    for (int cb = 0; cb < 3; ++cb) acc[k][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float gsc[KH_MAXC / 256], gsh[KH_MAXC / 256];
+  if constexpr (gn) {
+#pragma unroll
+    for (int k = 0; k < KH_MAXC / 256; ++k) {
+      const int i = tid + 256 * k;
+      if (i < Cin) {
+        gsc[k] = p.gn_scale[(size_t)b * Cin + i];
+        gsh[k] = p.gn_shift[(size_t)b * Cin + i];
+      }
+    }
+  }
+  KP_LOAD_H(0, hv);
+  KP_LOAD_W(0);
+  KP_LOAD_H(1, hw);
+  if (tid < (KP_PB * 16 - KH_HROWS) * 4)  // the padding rows past the halo: zeros (their partials are never read)
+    *(u32x4*)(halo + kh_swz(KH_HROWS + (tid >> 2), tid & 3)) = u32x4{0u, 0u, 0u, 0u};
+  if constexpr (gn) {
+#pragma unroll
+    for (int k = 0; k < KH_MAXC / 256; ++k) {
+      const int i = tid + 256 * k;
+      if (i < Cin) {
+        gtab[i] = GNM == 2 ? gsc[k] * kNegLog2e : gsc[k];  // gn_xform8's prescaled SiLU affine
+        gtab[Cin + i] = GNM == 2 ? gsh[k] * kNegLog2e : gsh[k];
+      }
+    }
+    __syncthreads();
+  }
+  auto step = [&](int c, u32x4 (&h)[KH_HJ]) {
+    float sc[8], sh[8];
+    if constexpr (gn) {
+      const float* gp = gtab + c * 32 + hcol * 8;
+      const f32x4 s0 = *(const f32x4*)gp, s1 = *(const f32x4*)(gp + 4);
+      const f32x4 t0 = *(const f32x4*)(gp + Cin), t1 = *(const f32x4*)(gp + Cin + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        sc[e] = s0[e]; sc[4 + e] = s1[e];
+        sh[e] = t0[e]; sh[4 + e] = t1[e];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KH_HJ; ++j) {
+      const int hr = (tid >> 2) + 64 * j;
+      if (j == KH_HJ - 1 && hr >= KH_HROWS) break;
+      u32x4 v = h[j];
+      if constexpr (gn) v = gn_xform8<GNM>(v, sc, sh, hok[j]);  // rows outside the image: the conv's zero padding
+      *(u32x4*)(halo + kh_swz(hr, hcol)) = v;
+    }
+    if (tid < 192) *(u32x4*)(wsl + kh_swz(tid >> 2, tid & 3)) = wv;  // 48 columns x 4 16-B chunks
+    KP_LOAD_W(c + 1);
+    KP_LOAD_H(c + 2, h);
+    __syncthreads();
+    // (the weight fragments are re-read per pixel block: 8 registers fewer than holding all three, which kept the
+    // kernel at three workgroups per CU without a spill -- a spill reload's vmcnt(0) waited on every halo load)
+#pragma unroll
+    for (int k = 0; k < KP_NB; ++k) {
+      const int pb = wid + 4 * k;
+      if (pb < KP_PB) {
+        const u32x4 a = *(const u32x4*)(halo + kh_swz(pb * 16 + lrow, lg));
+#pragma unroll
+        for (int cb = 0; cb < 3; ++cb)
+          acc[k][cb] = mfma_chunk<bf16_t>(a, *(const u32x4*)(wsl + kh_swz(cb * 16 + lrow, lg)), acc[k][cb]);
+      }
+    }
+    __syncthreads();
+  };
+  for (int c = 0; c < nc; c += 2) {  // nc is even: bf16 channels come in 64-channel K-tiles (snrse_conv2d)
+    step(c, hv);
+    step(c + 1, hw);
+  }
+  // the shifted sum: thread = output pixel (tile row r, column x), one 16-column block (taps 4 cb ..) at a time
+  float* const part = (float*)smem;
+  const int r = tid >> 5, x = tid & 31;
+  f32x4 y = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int cb = 0; cb < 3; ++cb) {
+#pragma unroll
+    for (int k = 0; k < KP_NB; ++k) {
+      const int pb = wid + 4 * k;
+      if (pb < KP_PB) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) part[(pb * 16 + lg * 4 + e) * KP_PS + lrow] = acc[k][cb][e];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int tap = 4 * cb + j;
+      if (tap < 9) {
+        const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+        y += *(const f32x4*)(part + ((r + dy + 1) * KH_HC + x + dx + 1) * KP_PS + 4 * j);
+      }
+    }
+    __syncthreads();
+  }
+  const size_t m = ((size_t)b * p.H + h0 + r) * p.W + w0 + x;
+  if (p.bias) y += f32x4{p.bias[0], p.bias[1], p.bias[2], p.bias[3]};
+  if (p.res) y += *(const f32x4*)((const float*)p.res + m * p.res_ld);
+  y *= p.out_scale;
+  *(f32x4*)((float*)p.out + m * p.out_ld) = y;
+}
+#undef KP_LOAD_W
+#undef KP_LOAD_H
 #undef KH_LOAD_H
 #undef KH_LOAD_W
 
@@ -492,10 +681,16 @@ bool head_ok(const ConvParams& p) {
   return p.bytes0 < lim && p.bytes1 < lim && p.wbytes < lim;
 }
 
-int launch_head(const ConvParams& p, hipStream_t s) {
+int launch_head(const ConvParams& p, hipStream_t s, bool part) {
   if (!head_ok(p)) return SNRSE_EINVAL;
   const long long tiles = (long long)p.B * (p.H / KH_TH) * (p.W / KH_TW);
   if (tiles <= 0 || tiles > 0x7fffffffLL) return SNRSE_EINVAL;
+  if (part && p.Cout == 4) {
+    if (!p.gn_scale) hipLaunchKernelGGL(conv_head_part_kernel<0>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+    else if (!p.gn_act) hipLaunchKernelGGL(conv_head_part_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL(conv_head_part_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+    return (int)hipGetLastError();
+  }
   if (!p.gn_scale) hipLaunchKernelGGL(conv_head_kernel<0>, dim3((unsigned)tiles), dim3(256), 0, s, p);
   else if (!p.gn_act) hipLaunchKernelGGL(conv_head_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, s, p);
   else hipLaunchKernelGGL(conv_head_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, s, p);

@@ -710,11 +710,13 @@ def test_glds_small_levels(gpu, B, C0, C1, Csc, H, W):
     assert rel(outs[1], outs[0]) < 1e-2
 
 
+@pytest.mark.parametrize("part", [1, 0])
 @pytest.mark.parametrize("shape", [(2, 128, 8, 64), (1, 256, 8, 128), (2, 128, 16, 32), (1, 256, 24, 96),
                                    (2, 192, 16, 64), (1, 64, 8, 32)])
-def test_conv_head_fused_groupnorm(gpu, shape):
+def test_conv_head_fused_groupnorm(gpu, shape, part):
     """Pyramid-head conv (C -> 4, f32 out, + upsampled pyramid) consuming SiLU(GN(h)) through the
-    halo-staged head kernel (ncsnpp.py:348-366), 2 .. 8 channel chunks."""
+    halo-staged head kernels (ncsnpp.py:348-366), 2 .. 8 channel chunks: the tap-partials form (option head_part
+    1, the default: a 1x1 GEMM of the halo into 36 tap partials, then their shifted sum) and the nine-tap form."""
     from snrse import ops
     B, C, H, W = shape
     x = (torch.from_numpy(fnormal("t.hd.x", (B, C, H, W))) * 1.5 + 0.2).bfloat16().float()
@@ -730,10 +732,18 @@ def test_conv_head_fused_groupnorm(gpu, shape):
     gn = ops.gn_scale_shift(sums, g.to(gpu), be.to(gpu), H * W)
     wp = torch.cat([w.permute(0, 2, 3, 1).reshape(4, -1), torch.zeros(12, 9 * C)]).to(gpu, torch.bfloat16).contiguous()
     assert ops.head_ok(xg)
-    out = ops.conv2d(xg, wp, 3, 4, bias=b.to(gpu), res=nhwc(r).to(gpu), out_f32=True, gn=gn)
-    assert ops.kernel_name(ops.get_option("last_kernel")) == "conv_head_kernel"
+    ops.set_option("head_part", part)
+    try:
+        out = ops.conv2d(xg, wp, 3, 4, bias=b.to(gpu), res=nhwc(r).to(gpu), out_f32=True, gn=gn)
+        assert ops.kernel_name(ops.get_option("last_kernel")) == ("conv_head_part_kernel" if part else "conv_head_kernel")
+        # no GroupNorm (the raw input), and the affine without SiLU, against the same kernel's contract
+        out0 = ops.conv2d(xg, wp, 3, 4, bias=b.to(gpu), out_f32=True)
+    finally:
+        ops.set_option("head_part", 1)
     assert out.dtype == torch.float32
     assert rel(nchw(out), ref) < 1e-2
+    ref0 = F.conv2d(x.double(), w.double(), b.double(), padding=1)
+    assert rel(nchw(out0), ref0) < 1e-2
 
 
 @pytest.mark.parametrize("split", [False, True])
