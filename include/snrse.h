@@ -152,7 +152,8 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  * "conv_variant" 0 auto, 1 register-staged v1, 2 LDS-DMA v2, 5 halo GEMM v5 (the default halo kernel);
  * "splitk" 0 disables the split-K small-image GEMMs, "splitk_target" workgroups a split launch aims for;
  * "epi_nt" 0 / 1 / 2 (auto above "epi_nt_mb" = 256 MB of output) non-temporal halo-GEMM output stores;
- * "h5_specialise" 1 compile-time epilogue flags for the NCSN++ ResBlock configurations;
+ * "h5_specialise" 1 compile-time epilogue flags for the NCSN++ ResBlock configurations (bf16 halo GEMM, and the
+ *   fp32x3 halo GEMM's pair schedule);
  * "h5_tw" halo-GEMM tile: 0 auto (8 rows x 32 px where H % 8 == 0, else 4 x 64), 64 forces 4 x 64;
  * "resample_variant" 0 row-strip / 1 LDS-tiled gn_resample, "resample_nt" non-temporal stores there,
  * "resample_down_rows" 1 / 2 / 4 (default) output rows per down-sampling row strip (bit-identical results);

@@ -122,7 +122,8 @@ struct snrse_ctx {
   int splitk_target = 256;     // workgroups a split-K launch aims for (C2 sweep: 256 best)
   int epi_nt = 2;              // halo-GEMM non-temporal output stores: 0 off, 1 on, 2 above epi_nt_mb
   int epi_nt_mb = 256;         // MB of output above which epi_nt = 2 streams (the Infinity Cache size)
-  int h5_specialise = 1;       // compile-time epilogue flags for the common bf16 configurations
+  int h5_specialise = 1;       // compile-time epilogue flags for the common bf16 (halo GEMM) and fp32x3 (x3h pair
+                               // schedule) ResBlock configurations
   int h5_tw = 0;               // halo tile width: 0 auto (32 where H % 8 == 0), 64, 32
   int stats_zeroed = 0;        // statistics buffers arrive zeroed (the caller clears one arena)
   int resample_variant = 0;    // 0 row-strip, 1 LDS-tiled gn_resample

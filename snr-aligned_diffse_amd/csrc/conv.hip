@@ -856,7 +856,7 @@ SNRSE_DEV void x3h_vm_wait(int n) {
 // the pair schedule: TW 32, an even number of main chunks) TWO taps per phase -- half the barriers -- over a 2-slot
 // ring of 2-tap weight slots, the main chunks in pairs (18 taps = 9 phases with compile-time taps), the next chunk's
 // halo pieces stored after its taps 2..7
-template <int GNM, int SPR, int TWV>
+template <int GNM, int SPR, int TWV, int EF = EF_RT>
 __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
   using G = X3G<TWV, SPR>;
   constexpr int TH = G::TH, TW = G::TW, HC = G::HC, HROWS = G::HROWS, HBYTES = G::HBYTES, HJ = G::HJ;
@@ -1266,7 +1266,7 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
     epilogue_lds<float, 4, 128>(p, acc, mb, n0 + wc * 64, lane, (float*)(smem + wid * (64 * 68 * 4)),
                                 (float*)(smem + 8 * (64 * 68 * 4)), wr, bb, n0, min(TW, p.W - w0));
   else  // two 32-px row segments per wave (W % 32 == 0: no cut tiles)
-    epilogue_img<float, 4, 128, false, EF_RT, TW>(p, acc, mb, n0 + wc * 64, lane, (float*)(smem + wid * (64 * 68 * 4)),
+    epilogue_img<float, 4, 128, false, EF, TW>(p, acc, mb, n0 + wc * 64, lane, (float*)(smem + wid * (64 * 68 * 4)),
                                                  (float*)(smem + 8 * (64 * 68 * 4)), wr, bb, n0, p.W - TW);
 }
 
@@ -2095,35 +2095,60 @@ int launch_x3(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   return (int)hipGetLastError();
 }
 
-template <int GNM, int SPR, int TWV>
-int launch_x3h_gn(ConvParams p, hipStream_t s, int tiles) {
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_x3h_kernel<GNM, SPR, TWV>,
+template <int GNM, int SPR, int TWV, int EF = EF_RT>
+int launch_x3h_ef(ConvParams p, hipStream_t s, int tiles) {
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_x3h_kernel<GNM, SPR, TWV, EF>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
                                                      (int)X3G<TWV, SPR>::LDS);
   SNRSE_RET(attr);
   p.ntn = p.Cout / 128;
   p.ksplit = 1;
   constexpr size_t lds = X3G<TWV, SPR>::LDS;
-  hipLaunchKernelGGL((conv_x3h_kernel<GNM, SPR, TWV>), dim3(tiles), dim3(512), lds, s, p);
+  hipLaunchKernelGGL((conv_x3h_kernel<GNM, SPR, TWV, EF>), dim3(tiles), dim3(512), lds, s, p);
   return (int)hipGetLastError();
 }
 
+template <int GNM, int SPR, int TWV>
+int launch_x3h_gn(const ConvParams& p, hipStream_t s, int tiles, bool spec) {
+  // the ResBlock convs of the fp32x3 path on the pair schedule (GroupNorm+SiLU prologue, or none after a resampler;
+  // 8 x 32 tiles) get a
+  // compile-time epilogue like the bf16 halo GEMM's: Conv_0 (+temb), Conv_1 (+residual, or the shortcut as extra K,
+  // + the down-sampling blocks' pyramid Combine), each with statistics, +-NT (fp32x3 C2 line +1.5 %,
+  // profiles/r05z / r05za_x3h_specialise_ab.jsonl)
+  if constexpr (GNM != 1 && SPR == 2 && TWV == 32) {
+    if (spec && p.bias) {
+      switch (epi_flags(p)) {
+        case EF_TEMB | EF_STATS: return launch_x3h_ef<GNM, SPR, TWV, EF_TEMB | EF_STATS>(p, s, tiles);
+        case EF_TEMB | EF_STATS | EF_NT: return launch_x3h_ef<GNM, SPR, TWV, EF_TEMB | EF_STATS | EF_NT>(p, s, tiles);
+        case EF_RES | EF_STATS: return launch_x3h_ef<GNM, SPR, TWV, EF_RES | EF_STATS>(p, s, tiles);
+        case EF_RES | EF_STATS | EF_NT: return launch_x3h_ef<GNM, SPR, TWV, EF_RES | EF_STATS | EF_NT>(p, s, tiles);
+        case EF_STATS: return launch_x3h_ef<GNM, SPR, TWV, EF_STATS>(p, s, tiles);
+        case EF_STATS | EF_NT: return launch_x3h_ef<GNM, SPR, TWV, EF_STATS | EF_NT>(p, s, tiles);
+        case EF_COMB | EF_STATS: return launch_x3h_ef<GNM, SPR, TWV, EF_COMB | EF_STATS>(p, s, tiles);
+        case EF_COMB | EF_STATS | EF_NT: return launch_x3h_ef<GNM, SPR, TWV, EF_COMB | EF_STATS | EF_NT>(p, s, tiles);
+        default: break;
+      }
+    }
+  }
+  return launch_x3h_ef<GNM, SPR, TWV>(p, s, tiles);
+}
+
 template <int SPR, int TWV>
-int launch_x3h_spr(const ConvParams& p, hipStream_t s, int tiles) {
-  if (!p.gn_scale) return launch_x3h_gn<0, SPR, TWV>(p, s, tiles);
-  if (!p.gn_act) return launch_x3h_gn<1, SPR, TWV>(p, s, tiles);
-  return launch_x3h_gn<2, SPR, TWV>(p, s, tiles);
+int launch_x3h_spr(const ConvParams& p, hipStream_t s, int tiles, bool spec) {
+  if (!p.gn_scale) return launch_x3h_gn<0, SPR, TWV>(p, s, tiles, spec);
+  if (!p.gn_act) return launch_x3h_gn<1, SPR, TWV>(p, s, tiles, spec);
+  return launch_x3h_gn<2, SPR, TWV>(p, s, tiles, spec);
 }
 
 // tw 32: the 8 x 32 px tiles (H % 8 == 0, W % 32 == 0; tiles counted for them), else 4 x 64
-int launch_x3h(const ConvParams& p, hipStream_t s, int tiles, int spread, int tw) {
+int launch_x3h(const ConvParams& p, hipStream_t s, int tiles, int spread, int tw, bool spec) {
   // the pair schedule (spread 2) needs 8 x 32 tiles and an even number of 32-channel main chunks
   if (spread == 2 && !(tw == 32 && ((p.C0 + p.C1) / 32) % 2 == 0)) spread = 1;
   if (tw == 32) {
-    if (spread == 2) return launch_x3h_spr<2, 32>(p, s, tiles);
-    return spread ? launch_x3h_spr<1, 32>(p, s, tiles) : launch_x3h_spr<0, 32>(p, s, tiles);
+    if (spread == 2) return launch_x3h_spr<2, 32>(p, s, tiles, spec);
+    return spread ? launch_x3h_spr<1, 32>(p, s, tiles, spec) : launch_x3h_spr<0, 32>(p, s, tiles, spec);
   }
-  return spread ? launch_x3h_spr<1, 64>(p, s, tiles) : launch_x3h_spr<0, 64>(p, s, tiles);
+  return spread ? launch_x3h_spr<1, 64>(p, s, tiles, spec) : launch_x3h_spr<0, 64>(p, s, tiles, spec);
 }
 
 template <int BM, int BN, typename TO>
@@ -2278,7 +2303,7 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
         const bool tw32 = cx.x3_tw != 64 && q.H % 8 == 0 && q.W % 32 == 0;
         cx.last_tw = tw32 ? 32 : 64;
         return launch_x3h(r, stream, tw32 ? q.B * (q.H / 8) * (q.W / 32) * (q.Cout / 128) : x3h_tiles, cx.x3_spread,
-                          tw32 ? 32 : 64);
+                          tw32 ? 32 : 64, cx.h5_specialise != 0);
       }
       if (q.Cout <= 16 && cx.conv_variant != 1 && head_ok(q)) {  // the pyramid heads, GroupNorm fused
         cx.last_kernel = 11;
