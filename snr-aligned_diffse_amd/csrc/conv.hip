@@ -269,10 +269,34 @@ SNRSE_DEV int epi_pix(int mb, int row, int seg_skip) {
   return TW == 64 ? mb + row : mb + row + (row / TW) * seg_skip;
 }
 
+// bias + temb of the lane's EPC channels of an epilogue_img call over channels nb .. nb + 63 of image b
+template <typename TO, int EF>
+SNRSE_DEV void epi_add(const ConvParams& p, int nb, int lane, int b, float (&add)[16 / sizeof(TO)]) {
+  constexpr int EPC = 16 / (int)sizeof(TO);
+  const int n = nb + (lane % (64 / EPC)) * EPC;
+  const bool f_temb = EF < 0 ? p.temb != nullptr : (EF & EF_TEMB) != 0;
+#pragma unroll
+  for (int k = 0; k < EPC; ++k) add[k] = 0.f;
+  if (p.bias) {  // (assigned, not added to 0: an add in the branch made the compiler wait for the load there)
+#pragma unroll
+    for (int k = 0; k < EPC; k += 4) {
+      const f32x4 v = *(const f32x4*)(p.bias + n + k);
+      add[k] = v[0]; add[k + 1] = v[1]; add[k + 2] = v[2]; add[k + 3] = v[3];
+    }
+  }
+  if (f_temb) {
+    const float* tb = p.temb + (size_t)b * p.temb_stride + n;
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) add[k] += tb[k];
+  }
+}
+
+// pre_add: the lane's bias + temb already loaded by the caller (epi_add), so its round trip overlaps the caller's
+// drain before the epilogue instead of following it (the halo GEMMs load both halves' up front)
 template <typename TO, int NWM, int BN, bool DEFER, int EF = EF_RT, int TW = 64, int LA = 8>
 SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int mb, int nb, int lane, float* stage,
-                            float* red, int wm, int b, int blk_n0, int seg_skip = 0) {
-  const bool f_temb = EF < 0 ? p.temb != nullptr : (EF & EF_TEMB) != 0;
+                            float* red, int wm, int b, int blk_n0, int seg_skip = 0,
+                            const float* pre_add = nullptr) {
   const bool f_res = EF < 0 ? p.res != nullptr : (EF & EF_RES) != 0;
   const bool f_comb = EF < 0 ? p.comb_src != nullptr : (EF & EF_COMB) != 0;
   const bool f_stats = EF < 0 ? p.stats != nullptr : (EF & EF_STATS) != 0;
@@ -291,19 +315,11 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
   const int cc = lane % NCH, r0 = lane / NCH;
   const int n = nb + cc * EPC;
   float add[EPC];
+  if (pre_add) {
 #pragma unroll
-  for (int k = 0; k < EPC; ++k) add[k] = 0.f;
-  if (p.bias) {  // (assigned, not added to 0: an add in the branch made the compiler wait for the load there)
-#pragma unroll
-    for (int k = 0; k < EPC; k += 4) {
-      const f32x4 v = *(const f32x4*)(p.bias + n + k);
-      add[k] = v[0]; add[k + 1] = v[1]; add[k + 2] = v[2]; add[k + 3] = v[3];
-    }
-  }
-  if (f_temb) {
-    const float* tb = p.temb + (size_t)b * p.temb_stride + n;
-#pragma unroll
-    for (int k = 0; k < EPC; ++k) add[k] += tb[k];
+    for (int k = 0; k < EPC; ++k) add[k] = pre_add[k];
+  } else {
+    epi_add<TO, EF>(p, nb, lane, b, add);
   }
   float cw[EPC][4], cb[EPC];
   if (f_comb) {
@@ -1922,6 +1938,10 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   }
   }
   SNRSE_STAMP(28);
+  // both epilogue halves' bias + temb, requested before the drain below so that their round trip overlaps it
+  float add0[16 / sizeof(TO)], add1[16 / sizeof(TO)];
+  epi_add<TO, EF>(p, n0, lane, bb, add0);
+  epi_add<TO, EF>(p, n0 + 64, lane, bb, add1);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // (the out-of-range DMA after the last phase too)
   __builtin_amdgcn_s_barrier();  // LDS is reused as the epilogue staging area
   float* const stage = (float*)(smem + wid * (64 * 68 * 4));
@@ -1929,11 +1949,11 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   const int mrow = (bb * p.H + h0 + wid * RW) * p.W + w0;
   // (f32 output, the exact mode: residuals two passes ahead -- acc[1] is still live here, 256 registers)
   constexpr int ELA = sizeof(TO) == 2 ? 8 : 2;
-  epilogue_img<TO, 4, 128, true, EF, TW, ELA>(p, acc[0], mrow, n0, lane, stage, red, wid, bb, n0, p.W - TW);
+  epilogue_img<TO, 4, 128, true, EF, TW, ELA>(p, acc[0], mrow, n0, lane, stage, red, wid, bb, n0, p.W - TW, add0);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
   SNRSE_STAMP(26);
-  epilogue_img<TO, 4, 128, true, EF, TW, ELA>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0, p.W - TW);
+  epilogue_img<TO, 4, 128, true, EF, TW, ELA>(p, acc[1], mrow, n0 + 64, lane, stage, red, wid, bb, n0, p.W - TW, add1);
   SNRSE_STAMP(27);
   if (EF < 0 ? p.stats != nullptr : (EF & EF_STATS) != 0) block_stats_flush<4, 128>(p, red, bb, n0);
 #ifdef SNRSE_STAMPS
