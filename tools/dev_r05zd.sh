@@ -1,0 +1,12 @@
+# r05zd: the halo GEMM epilogue's bias + temb loads of both halves all issued before the first add (one round trip
+# before the drain instead of two): GPU suite, ABAB of the bf16 line against HEAD's library (var_base)
+O=$PWD/gpurun_out/r05zd
+R=$GRAFT_REPO_ROOT
+B=$R/snr-aligned_diffse_amd/lib/var_base/libsnrse_hip.so
+L="python -u bench.py --no-cpu-baseline --no-parity-mode --steps 10 --warmup 3"
+bash tools/gpu_step.sh $O \
+ "tests:::600:::cd $R && python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread" \
+ "bf_new1:::200:::cd $R && $L > $O/bf_new1.json" \
+ "bf_base1:::200:::cd $R && SNRSE_LIB=$B $L > $O/bf_base1.json" \
+ "bf_new2:::200:::cd $R && $L > $O/bf_new2.json" \
+ "bf_base2:::200:::cd $R && SNRSE_LIB=$B $L > $O/bf_base2.json"
