@@ -242,6 +242,70 @@ def test_x3h_fused_groupnorm_silu(gpu, shape, act, spread):
     assert rel(nchw(out), ref) < TOL
 
 
+@pytest.mark.parametrize("nt", [0, 1])
+@pytest.mark.parametrize("gnm", [2, 0])
+@pytest.mark.parametrize("flags", ["temb", "res", "comb", "shortcut"])
+def test_x3h_specialised_epilogue_matches_runtime_flags(gpu, flags, gnm, nt):
+    """The pair schedule's compile-time epilogue variants (option h5_specialise 1, the default: GroupNorm+SiLU or
+    none, + temb / residual / Combine / the shortcut as extra K, with statistics, +-NT) against the run-time-flag
+    kernel (h5_specialise 0) on the same inputs -- same arithmetic, so equal to 1e-6 -- and against fp64."""
+    from snrse import ops
+    B, cin, cout, H, W = 2, 128, 128, 8, 64
+    x = torch.from_numpy(fnormal("t.xs.x", (B, cin, H, W))) * 1.5 + 0.2
+    w = torch.from_numpy(fnormal("t.xs.w", (cout, cin, 3, 3))) / math.sqrt(9 * cin)
+    b = torch.from_numpy(fnormal("t.xs.b", (cout,)))
+    g = torch.from_numpy(fnormal("t.xs.g", (cin,))) * 0.1 + 1
+    be = torch.from_numpy(fnormal("t.xs.be", (cin,))) * 0.1
+    a = x.double()
+    if gnm:
+        a = F.silu(F.group_norm(a, min(cin // 4, 32), g.double(), be.double(), eps=1e-6))
+    ref = F.conv2d(a, w.double(), b.double(), padding=1)
+    xg = nhwc(x).to(gpu)
+    kw = {}
+    if gnm:
+        sums = ops.gn_stats(xg)
+        kw.update(gn=ops.gn_scale_shift(sums[0], g.to(gpu), be.to(gpu), H * W), gn_act=True)
+    if flags == "temb":
+        temb = torch.from_numpy(fnormal("t.xs.temb", (B, 200)))
+        ref = ref + temb[:, 8:8 + cout, None, None].double()
+        kw.update(temb=temb.to(gpu), temb_off=8)
+    elif flags == "res":
+        r = torch.from_numpy(fnormal("t.xs.r", (B, cout, H, W)))
+        ref = (ref + r.double()) / math.sqrt(2)
+        kw.update(res=nhwc(r).to(gpu), out_scale=1 / math.sqrt(2))
+    elif flags == "comb":
+        pyr = torch.from_numpy(fnormal("t.xs.pyr", (B, 4, H, W)))
+        cw = torch.from_numpy(fnormal("t.xs.cw", (cout, 4)))
+        cb = torch.from_numpy(fnormal("t.xs.cb", (cout,)))
+        ref = ref + torch.einsum("bihw,oi->bohw", pyr.double(), cw.double()) + cb.double()[None, :, None, None]
+        kw.update(comb=nhwc(pyr).to(gpu), comb_w=cw.to(gpu), comb_b=cb.to(gpu))
+    else:
+        xs = torch.from_numpy(fnormal("t.xs.xs", (B, 64, H, W)))
+        w2 = torch.from_numpy(fnormal("t.xs.w2", (cout, 64, 1, 1))) / 8
+        ref = ref + F.conv2d(xs.double(), w2.double())
+        kw.update(sc=nhwc(xs).to(gpu), sc_wgt=ops.split_weight(w2.reshape(cout, 64).to(gpu)))
+    wp = ops.split_weight(w.permute(0, 2, 3, 1).reshape(cout, -1).to(gpu))
+    outs, sts = {}, {}
+    ops.set_option("x3_tile", 4)
+    ops.set_option("epi_nt", nt)
+    try:
+        for spec in (1, 0):
+            ops.set_option("h5_specialise", spec)
+            sts[spec] = ops.new_stats(B, cout)
+            outs[spec] = ops.conv2d(xg, wp, 3, cout, bias=b.to(gpu), stats=sts[spec], **kw)
+            assert ops.get_option("last_kernel") == 4
+            assert ops.get_option("last_epi_nt") == nt
+    finally:
+        ops.set_option("x3_tile", 0)
+        ops.set_option("epi_nt", 2)
+        ops.set_option("h5_specialise", 1)
+    assert rel(outs[1], outs[0]) < 1e-6
+    assert rel(ops.fold_stats(sts[1]), ops.fold_stats(sts[0])) < 1e-6
+    assert rel(nchw(outs[1]), ref) < TOL
+    o = outs[1].double()
+    assert rel(ops.fold_stats(sts[1]), torch.stack([o.sum((1, 2)), (o * o).sum((1, 2))], -1)) < 1e-5
+
+
 @pytest.fixture(scope="module")
 def net_x3(gpu):
     from snrse import ncsnpp
