@@ -36,7 +36,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "utterances/sec (4 s @16 kHz, N=30 PC steps) at 1/2/4/8 MI355X; PESQ delta vs ref"
-PEAK = {"bf16": 2.5e15, "fp32": 157.3e12,  # dense MFMA peaks (MI355X_MICROARCH.md)
+PEAK = {"fp16": 2.5e15, "bf16": 2.5e15, "fp32": 157.3e12,  # dense MFMA peaks (MI355X_MICROARCH.md)
         "fp32x3": 2.5e15 / 3}  # split-bf16 fp32 GEMM: three dense bf16 MFMA products per fp32 product
 SR = 16000
 
@@ -498,8 +498,20 @@ def run_train(args):
 
 
 # ----------------------------------------------------------------------------- GPU bench
-CONFIG_DEFAULTS = {"c2": dict(batch=32, N=30, seconds=4.0, dtype="bf16"),
-                   "c4": dict(batch=32, N=30, seconds=4.0, dtype="bf16"),
+def roctx_region():
+    """f(True) / f(False): roctxProfilerResume(0) / roctxProfilerPause(0) around the timed steps when SNRSE_ROCTX=1, so
+    `rocprofv3 --selected-regions` collects exactly the timed kernels; a no-op otherwise."""
+    if os.environ.get("SNRSE_ROCTX") != "1":
+        return lambda on: None
+    import ctypes
+    lib = ctypes.CDLL("librocprofiler-sdk-roctx.so")
+    return lambda on: (lib.roctxProfilerResume if on else lib.roctxProfilerPause)(ctypes.c_uint64(0))
+
+
+# c2 / c4: the configuration's 16-bit arithmetic, in IEEE fp16 since round 6 (same bytes and MFMA rate as bf16;
+# bf16 misses SURVEY 8(c)'s 1e-2 parity bound, fp16 meets it: DESIGN.md 9, profiles/r06a_bf16_attribution.jsonl)
+CONFIG_DEFAULTS = {"c2": dict(batch=32, N=30, seconds=4.0, dtype="fp16"),
+                   "c4": dict(batch=32, N=30, seconds=4.0, dtype="fp16"),
                    "c5": dict(batch=1, N=200, seconds=30.0, dtype="fp32"),
                    "train": dict(batch=8, N=30, seconds=4.0, dtype="fp32")}
 
@@ -517,7 +529,7 @@ def run(args):
     from snrse.enhance import PCEnhancer
 
     ops.set_option("conv_variant", args.conv_variant)
-    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    dtype = {"fp16": torch.float16, "bf16": torch.bfloat16}.get(args.dtype, torch.float32)
     net = ncsnpp.NCSNppHIP(formula_weights(), dtype=dtype, device=dev, gemm="x3" if args.dtype == "fp32x3" else "exact")
     sde = sampler.SDESpec("ouve", theta=1.5, sigma_min=0.05, sigma_max=0.5)
     enh = PCEnhancer(net, sde, N=args.N, streams=args.streams, stagger=bool(args.stagger))
@@ -540,12 +552,15 @@ def run(args):
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    region = roctx_region()  # (rocprofv3 --selected-regions: the kernel summary brackets exactly the timed steps)
+    region(True)
     t0 = time.perf_counter()
     for k in range(args.steps):
         xh, nfe = enh(y, noise(100 + k))
         if rank == 0 and args.steps > 1:
             print(f"[bench] step {k + 1}/{args.steps} enqueued", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
+    region(False)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -616,7 +631,7 @@ def run(args):
     # N=5 PC golden check (halo kernel forced at the golden's size) and the C2-size agreement of the timed
     # bf16 output with the x3 output of the same clips and Philox seed (c2_agreement)
     pmode = None
-    if (world == 1 and args.config == "c2" and args.dtype == "bf16" and not args.no_parity_mode
+    if (world == 1 and args.config == "c2" and args.dtype in ("fp16", "bf16") and not args.no_parity_mode
             and args.seconds == 4.0 and args.N == 30):
         del enh, probe_enh, net
         torch.cuda.empty_cache()
@@ -627,20 +642,21 @@ def run(args):
         torch.cuda.synchronize()
         t3 = time.perf_counter()
         for k in range(K3):
-            xh3, _ = enh3(y, noise(100 + k))  # the bf16 timed steps' seeds
+            xh3, _ = enh3(y, noise(100 + k))  # the 16-bit timed steps' seeds
         torch.cuda.synchronize()
         el3 = time.perf_counter() - t3
         pmode = {"dtype": "fp32x3", "value": K3 * B / el3, "unit": "utt/s", "ms_per_step": el3 / K3 * 1e3,
                  "steps": K3, "warmup": 1,
                  "note": ("fp32 activations / storage / accumulation, ResBlock and input convs as "
                           "split-bf16 GEMMs (bench.py --dtype fp32x3 for the full line)")}
-        # the x3 output for the bf16 timed run's last seed (100 + steps - 1): the K3-th timed step when
+        # the x3 output for the 16-bit timed run's last seed (100 + steps - 1): the K3-th timed step when
         # K3 == steps, else one more untimed step
         if K3 != args.steps:
             xh3, _ = enh3(y, noise(100 + args.steps - 1))
         import paritycheck
-        pmode["c2_agreement"] = paritycheck.waveform_agreement(xh, xh3)
-        pmode["c2_agreement"]["what"] = (f"timed bf16 C2 output vs fp32x3 on the same {B} clips and Philox seed "
+        pmode["c2_agreement"] = paritycheck.waveform_agreement(
+            xh, xh3, bounds=paritycheck.C2_AGREE16 if args.dtype == "fp16" else paritycheck.C2_AGREE)
+        pmode["c2_agreement"]["what"] = (f"timed {args.dtype} C2 output vs fp32x3 on the same {B} clips and Philox seed "
                                          f"(N={args.N}, {nfe} NFE/utt)")
         if not args.no_probe:
             probe = ConvProbe()
@@ -726,19 +742,20 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", choices=["c2", "c4", "c5", "train"], default="c2",
-                    help="c2: PC sampler, B=32 4 s bf16 (default, the headline line); c4: one-step SNR-aligned "
+                    help="c2: PC sampler, B=32 4 s fp16 (default, the headline line); c4: one-step SNR-aligned "
                          "path (SNRNet estimate + 1 preconditioned NFE, sebridge_v3); c5: 30 s clips, N=200, fp32; "
                          "train: the consistency-training step (SURVEY §8(f) 2)")
     ap.add_argument("--frames", type=int, default=256, help="spectrogram frames of a training sample (--config train)")
     ap.add_argument("--batch", type=int, default=None, help="utterances per GPU")
     ap.add_argument("--N", type=int, default=None, help="PC steps")
     ap.add_argument("--seconds", type=float, default=None)
-    ap.add_argument("--dtype", choices=["bf16", "fp32", "fp32x3"], default=None,
-                    help="bf16; fp32 (exact fp32 MFMA GEMMs); fp32x3 (fp32 activations, split-bf16 GEMMs)")
+    ap.add_argument("--dtype", choices=["fp16", "bf16", "fp32", "fp32x3"], default=None,
+                    help="fp16 (c2 / c4 default); bf16 (the same kernels on bf16); fp32 (exact fp32 MFMA GEMMs); "
+                         "fp32x3 (fp32 activations, split-bf16 GEMMs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true")
     ap.add_argument("--no-parity-mode", action="store_true",
-                    help="skip the fp32x3 parity-mode step timed beside the default bf16 C2 line")
+                    help="skip the fp32x3 parity-mode step timed beside the default 16-bit C2 line")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the post-run parity check of the benched network vs tests/golden/pc_ouve.npz")
     ap.add_argument("--conv-variant", type=int, default=0, help="snrse conv_variant option (0 = auto)")

@@ -15,8 +15,10 @@
  *   - Return 0 on success or a hipError_t code (hipErrorInvalidValue = 1 for a bad
  *     argument); snrse_error_string() maps it to text.  The Python host maps non-zero to
  *     RuntimeError, as the reference's TORCH_CHECK does (op/upfirdn2d.cpp:8-19).
- *   - dtype: SNRSE_F32 = 0 (exact fp32 "parity" mode), SNRSE_BF16 = 1 (bf16 storage,
- *     fp32 accumulation), SNRSE_F32X3 = 4 (snrse_conv2d only: fp32 activations and output, weights
+ *   - dtype: SNRSE_F32 = 0 (exact fp32 "parity" mode), SNRSE_F16 = 2 (IEEE fp16 storage and MFMA
+ *     operands, fp32 accumulation: the 16-bit fast path's default since round 6, whose error against the
+ *     reference is ~9x below bf16's), SNRSE_BF16 = 1 (the same kernels on bf16; every entry
+ *     that takes SNRSE_BF16 takes SNRSE_F16 too), SNRSE_F32X3 = 4 (snrse_conv2d only: fp32 activations and output, weights
  *     pre-split into bf16 hi / lo halves, three bf16 MFMA products per K-tile -- the fast fp32
  *     parity mode).  Activations are NHWC: [B, F(=H), T(=W), C].
  *   - Complex spectrograms are interleaved complex64 [B, F, T] (= the reference's
@@ -152,7 +154,7 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  * "conv_variant" 0 auto, 1 register-staged v1, 2 LDS-DMA v2, 5 halo GEMM v5 (the default halo kernel);
  * "splitk" 0 disables the split-K small-image GEMMs, "splitk_target" workgroups a split launch aims for;
  * "epi_nt" 0 / 1 / 2 (auto above "epi_nt_mb" = 256 MB of output) non-temporal halo-GEMM output stores;
- * "h5_specialise" 1 compile-time epilogue flags for the NCSN++ ResBlock configurations (bf16 halo GEMM, and the
+ * "h5_specialise" 1 compile-time epilogue flags for the NCSN++ ResBlock configurations (16-bit halo GEMM, and the
  *   fp32x3 halo GEMM's pair schedule);
  * "h5_tw" halo-GEMM tile: 0 auto (8 rows x 32 px where H % 8 == 0, else 4 x 64), 64 forces 4 x 64;
  * "resample_variant" 0 row-strip / 1 LDS-tiled gn_resample, "resample_nt" non-temporal stores there,
@@ -203,13 +205,13 @@ int snrse_temb_gfp_dense(const float* t, const float* Wg, const float* W1, const
 int snrse_temb_dense(const float* temb, const float* W, const float* bias, float* out, int B, int R, int D,
                      hipStream_t stream);
 
-/* Fused input conv, bf16 (ncsnpp.py:253-254, 282-285): complex x, y [B][H][W] -> out [B*H*W][128]
- * bf16 = conv3x3(cat(x.re, x.im, y.re, y.im), wgt) + bias, plus the f32 input pyramid
+/* Fused input conv, 16-bit (ncsnpp.py:253-254, 282-285): complex x, y [B][H][W] -> out [B*H*W][128]
+ * (dtype SNRSE_F16 or SNRSE_BF16) = conv3x3(cat(x.re, x.im, y.re, y.im), wgt) + bias, plus the f32 input pyramid
  * pyr [B*H*W][4] and out's GroupNorm statistics [B][SLOTS][128][2] (zeroed here unless option
- * stats_zeroed).  wgt: bf16 [128][64], k = (ky * 3 + kx) * 4 + channel, k >= 36 zero.
+ * stats_zeroed).  wgt: dtype [128][64], k = (ky * 3 + kx) * 4 + channel, k >= 36 zero.
  * Requires W % 64 == 0 and (H * W / 64) % 16 == 0 (else SNRSE_EINVAL: use snrse_input_pack). */
 int snrse_input_conv(snrse_ctx* ctx, const void* x, const void* y, int B, int H, int W, const void* wgt, const float* bias,
-                     void* out, float* pyr, double* stats, hipStream_t stream);
+                     void* out, float* pyr, double* stats, int dtype, hipStream_t stream);
 
 /* The same input conv for the fp32x3 parity mode: wgt = ops.split_weight of the packed [128][64] weights ([128][128]
  * bf16: per 32-element K tile 32 hi then 32 lo), split-bf16 products (w_hi.x_hi + w_lo.x_hi + w_hi.x_lo), f32 out

@@ -7,7 +7,7 @@
 //
 // One wave owns 16 query rows; K/V tiles of KB keys are staged once per block in LDS and
 // shared by its waves.  S = Q K^T and O += P V both run on MFMA (16x16x32 bf16 or exact
-// 16x16x4 f32); the softmax is online (running max / sum per row), so the L x L score
+// 16x16x4 f32; fp16 as bf16); the softmax is online (running max / sum per row), so the L x L score
 // matrix is never materialised (L = 3776 for a 30 s clip).
 #include "common.h"
 
@@ -15,6 +15,7 @@ namespace {
 
 template <typename T> struct AttnCfg;
 template <> struct AttnCfg<bf16_t> { static constexpr int KT = 64, EPC = 8, NW = 4, KB = 64; };
+template <> struct AttnCfg<f16_t> { static constexpr int KT = 64, EPC = 8, NW = 4, KB = 64; };
 template <> struct AttnCfg<float> { static constexpr int KT = 32, EPC = 4, NW = 2, KB = 32; };
 
 SNRSE_DEV int swz(int row, int chunk) { return (row << 7) + ((chunk ^ ((row >> 1) & 7)) << 4); }
@@ -22,8 +23,7 @@ SNRSE_DEV int swz(int row, int chunk) { return (row << 7) + ((chunk ^ ((row >> 1
 template <typename T>
 SNRSE_DEV f32x4 mfma_chunk(const u32x4& a, const u32x4& b, f32x4 acc) {
   if constexpr (sizeof(T) == 2) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, a),
-                                                   __builtin_bit_cast(bf16x8_mfma, b), acc, 0, 0, 0);
+    return H16<T>::mfma(a, b, acc);
   } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(64 * AttnCfg<T>::NW) void attn_kernel(const T* qkv,
   for (int e = 0; e < 4; ++e) { m_run[e] = -INFINITY; l_run[e] = 0.f; }
 
   char* Pw = Ps + wid * P_BYTES;
-  // bf16: the next K / V block is loaded into registers while the current one is consumed, and V is
+  // 16-bit: the next K / V block is loaded into registers while the current one is consumed, and V is
   // transposed in registers (8 keys x 8 channels per thread, v_perm) so it lands in LDS as 16-B stores
   // (the per-element 2-B stores of the generic path held the level-4 attention at ~67 us;
   // profiles/r05a_c2_dispatch_shapes.jsonl)
@@ -434,6 +434,7 @@ __global__ __launch_bounds__(256) void attn_x3_kernel(const float* qkv, float* o
 extern "C" int snrse_attention(const void* qkv, void* out, int B, int L, int C, int dtype, hipStream_t stream) {
   if (!qkv || !out || L <= 0 || B <= 0) return SNRSE_EINVAL;
   if (C != 256) return SNRSE_EINVAL;  // NCSN++ attention runs at 256 channels (ncsnpp.py:170-171)
+  if (dtype == SNRSE_F16) return launch_attn<f16_t, 256>(qkv, out, B, L, stream);
   if (dtype == SNRSE_BF16) return launch_attn<bf16_t, 256>(qkv, out, B, L, stream);
   if (dtype == SNRSE_F32) return launch_attn<float, 256>(qkv, out, B, L, stream);
   if (dtype == SNRSE_F32X3) {  // fp32 in / out, split-bf16 products (the fp32x3 parity mode)

@@ -30,6 +30,57 @@ SNRSE_DEV uint32_t pack_bf16x2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
+// IEEE binary16 storage: the 16-bit fast path's format since round 6 (8 more significand bits' worth of
+// accuracy than bf16 at the same bytes and the same MFMA rate; bf16 missed SURVEY 8(c)'s 1e-2 bound,
+// profiles/r06a_bf16_attribution.jsonl).  A distinct type, so a kernel's format template argument picks the
+// conversions and the MFMA.
+struct f16_t {
+  uint16_t bits;
+};
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_mfma;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_t;
+
+// The two 16-bit formats: the halves of a packed 32-bit word, the packing convert (round to nearest even:
+// v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32) and the 16x16x32 MFMA with fp32 accumulation.
+template <typename T> struct H16;
+template <> struct H16<bf16_t> {
+  SNRSE_DEV static float lo(uint32_t v) { return __uint_as_float(v << 16); }
+  SNRSE_DEV static float hi(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
+  SNRSE_DEV static uint32_t pack(float a, float b) { return pack_bf16x2(a, b); }
+  SNRSE_DEV static f32x4 mfma(const u32x4& a, const u32x4& b, f32x4 acc) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_mfma, a),
+                                                   __builtin_bit_cast(bf16x8_mfma, b), acc, 0, 0, 0);
+  }
+};
+template <> struct H16<f16_t> {
+  SNRSE_DEV static float lo(uint32_t v) { return (float)__builtin_bit_cast(f16x2_t, v)[0]; }
+  SNRSE_DEV static float hi(uint32_t v) { return (float)__builtin_bit_cast(f16x2_t, v)[1]; }
+  SNRSE_DEV static uint32_t pack(float a, float b) {
+    const f16x2_t v = {(_Float16)a, (_Float16)b};
+    return __builtin_bit_cast(uint32_t, v);
+  }
+  SNRSE_DEV static f32x4 mfma(const u32x4& a, const u32x4& b, f32x4 acc) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_mfma, a),
+                                                  __builtin_bit_cast(f16x8_mfma, b), acc, 0, 0, 0);
+  }
+};
+// a 16-B vector of 8 16-bit values <-> 8 floats
+template <typename T>
+SNRSE_DEV void unpack8(const u32x4& r, float* v) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = H16<T>::lo(r[i]);
+    v[2 * i + 1] = H16<T>::hi(r[i]);
+  }
+}
+template <typename T>
+SNRSE_DEV u32x4 pack8(const float* v) {
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = H16<T>::pack(v[2 * i], v[2 * i + 1]);
+  return r;
+}
+
 template <typename T> struct Elem;
 template <> struct Elem<float> {
   static constexpr int kBytes = 4;
@@ -40,6 +91,11 @@ template <> struct Elem<bf16_t> {
   static constexpr int kBytes = 2;
   SNRSE_DEV static float to_f(bf16_t v) { return bf2f(v); }
   SNRSE_DEV static bf16_t from_f(float v) { return f2bf(v); }
+};
+template <> struct Elem<f16_t> {
+  static constexpr int kBytes = 2;
+  SNRSE_DEV static float to_f(f16_t v) { return (float)__builtin_bit_cast(_Float16, v.bits); }
+  SNRSE_DEV static f16_t from_f(float v) { return f16_t{__builtin_bit_cast(uint16_t, (_Float16)v)}; }
 };
 
 // bf16-path SiLU: v_exp_f32 + v_rcp_f32 (1 ulp) instead of an IEEE division (~10 VALU ops);
@@ -102,8 +158,10 @@ SNRSE_DEV double wave_sum_d(double v) {
 }
 
 // dtype codes shared with the C-ABI (include/snrse.h)
-// F16 / F64: snrse_upfirdn2d only; F32X3: snrse_conv2d's split-bf16 fp32 GEMM (pre-split weights)
+// F16 (round 6): the 16-bit fast path's default format, like BF16 on every 16-bit entry; F64: snrse_upfirdn2d
+// only; F32X3: snrse_conv2d's split-bf16 fp32 GEMM (pre-split weights)
 enum { SNRSE_F32 = 0, SNRSE_BF16 = 1, SNRSE_F16 = 2, SNRSE_F64 = 3, SNRSE_F32X3 = 4 };
+inline bool snrse_is16(int dtype) { return dtype == SNRSE_BF16 || dtype == SNRSE_F16; }
 
 // GroupNorm statistics buffers are [B][SNRSE_STAT_SLOTS][C][2] doubles: producers spread
 // their atomics over the slots (a few hundred workgroups per image would otherwise queue on

@@ -172,8 +172,8 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
       if constexpr (sizeof(TO) == 2) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          v[2 * k] += __uint_as_float(rv[k] << 16);
-          v[2 * k + 1] += __uint_as_float(rv[k] & 0xffff0000u);
+          v[2 * k] += H16<TO>::lo(rv[k]);
+          v[2 * k + 1] += H16<TO>::hi(rv[k]);
         }
       } else {
 #pragma unroll
@@ -190,7 +190,7 @@ SNRSE_DEV void epilogue_lds(const ConvParams& p, const f32x4 (&acc)[4][4], int m
     u32x4 o;
     if constexpr (sizeof(TO) == 2) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = (uint32_t)f2bf(v[2 * k]) | ((uint32_t)f2bf(v[2 * k + 1]) << 16);
+      for (int k = 0; k < 4; ++k) o[k] = H16<TO>::pack(v[2 * k], v[2 * k + 1]);
     } else {
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] = __float_as_uint(v[k]);
@@ -364,8 +364,8 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
       if constexpr (sizeof(TO) == 2) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          v[2 * k] += __uint_as_float(rv[k] << 16);
-          v[2 * k + 1] += __uint_as_float(rv[k] & 0xffff0000u);
+          v[2 * k] += H16<TO>::lo(rv[k]);
+          v[2 * k + 1] += H16<TO>::hi(rv[k]);
         }
       } else {
 #pragma unroll
@@ -384,7 +384,7 @@ SNRSE_DEV void epilogue_img(const ConvParams& p, const f32x4 (&acc)[4][4], int m
     u32x4 o;
     if constexpr (sizeof(TO) == 2) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = pack_bf16x2(v[2 * k], v[2 * k + 1]);
+      for (int k = 0; k < 4; ++k) o[k] = H16<TO>::pack(v[2 * k], v[2 * k + 1]);
     } else {
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] = __float_as_uint(v[k]);
@@ -934,9 +934,6 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
 #pragma unroll
     for (int j = 0; j < HJ; ++j) {
       const int voff = hok[j] ? (hpix[j] * cs + cc + hch * 4) * 4 : (int)0x80000000;  // outside: zero padding
-#ifdef X3H_EXP_NOHALO  // timing diagnostics only (results wrong): no halo loads after the first chunk
-      if (c > 0) { hv[j] = u32x4{(uint32_t)voff, 0u, 0u, 0u}; continue; }
-#endif
       hv[j] = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
     }
     if constexpr (GNM > 0) {  // issued for shortcut chunks too (unused there): a fixed count per prefetch
@@ -982,13 +979,6 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
     float x[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) x[k] = __uint_as_float(hv[j][k]);
-#ifdef X3H_EXP_NOXF  // timing diagnostics only (results wrong): the halo stored without GroupNorm / split VALU
-    if (j < HJ - 1 || hr < HROWS) {
-      *(u32x2*)(hb + swz(hr, hch >> 1) + (hch & 1) * 8) = u32x2{hv[j][0], hv[j][1]};
-      *(u32x2*)(hb + swz(hr, 4 + (hch >> 1)) + (hch & 1) * 8) = u32x2{hv[j][2], hv[j][3]};
-    }
-    return;
-#endif
     if constexpr (GNM > 0) {
       const uint32_t keep = tr ? 0u : ~0u, zero = (hok[j] || !tr) ? ~0u : 0u;
 #pragma unroll
@@ -1202,9 +1192,6 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
         if (tp == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + HOPS) : "memory");
         else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#ifdef X3H_EXP_BAR3  // timing diagnostics only (results wrong): a barrier every third tap instead of every tap
-        if (tp % 3 == 0)
-#endif
         __builtin_amdgcn_s_barrier();
         wload(q + 2);
         if (tp == 0) halo_load(c + 1 < ncb ? c + 1 : c);
@@ -1274,9 +1261,6 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // LDS is reused as the epilogue staging area
-#ifdef X3H_EXP_NOEPI  // timing diagnostics: the epilogue exists but is skipped at run time (out_scale never equals this)
-  if (p.out_scale != 12345.f) return;
-#endif
   const int mb = (bb * p.H + h0 + wr * RW) * p.W + w0;
   if constexpr (TW == 64)
     epilogue_lds<float, 4, 128>(p, acc, mb, n0 + wc * 64, lane, (float*)(smem + wid * (64 * 68 * 4)),
@@ -1293,7 +1277,7 @@ __global__ __launch_bounds__(512) void conv_x3h_kernel(ConvParams p) {
 // buffer's range check (an out-of-range voffset loads 0).  The LDS image is lane-linear per
 // DMA instruction; the chunk swizzle is applied to the per-lane SOURCE address and the
 // same XOR on the ds_read (conflict-free 16-row fragment reads).
-template <int BM, int BN, typename TO>
+template <int BM, int BN, typename T, typename TO>
 __global__ __launch_bounds__(512) void conv_glds_kernel(ConvParams p) {
   constexpr int WM = BM / 64, WN = BN / 64;
   static_assert(WM * WN == 8, "8 waves");
@@ -1434,7 +1418,7 @@ __global__ __launch_bounds__(512) void conv_glds_kernel(ConvParams p) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<bf16_t>(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<T>(af[i], bfr[j], acc[i][j]);
     }
     stage = stage == STAGES - 1 ? 0 : stage + 1;
   }
@@ -1522,11 +1506,11 @@ __global__ __launch_bounds__(256) void conv_splitk_finalize(ConvParams p, int pp
     }
     if (p.res) {
       if constexpr (sizeof(TO) == 2) {
-        const u32x4 rv = *(const u32x4*)((const bf16_t*)p.res + m * p.res_ld + n);
+        const u32x4 rv = *(const u32x4*)((const TO*)p.res + m * p.res_ld + n);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          v[2 * k] += __uint_as_float(rv[k] << 16);
-          v[2 * k + 1] += __uint_as_float(rv[k] & 0xffff0000u);
+          v[2 * k] += H16<TO>::lo(rv[k]);
+          v[2 * k + 1] += H16<TO>::hi(rv[k]);
         }
       } else {
         const float* rp = (const float*)p.res + m * p.res_ld + n;
@@ -1544,8 +1528,8 @@ __global__ __launch_bounds__(256) void conv_splitk_finalize(ConvParams p, int pp
     if constexpr (sizeof(TO) == 2) {
       u32x4 o;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = pack_bf16x2(v[2 * k], v[2 * k + 1]);
-      *(u32x4*)((bf16_t*)p.out + m * p.out_ld + n) = o;
+      for (int k = 0; k < 4; ++k) o[k] = H16<TO>::pack(v[2 * k], v[2 * k + 1]);
+      *(u32x4*)((TO*)p.out + m * p.out_ld + n) = o;
     } else {
       float* op = (float*)p.out + m * p.out_ld + n;
 #pragma unroll
@@ -1583,15 +1567,6 @@ __global__ __launch_bounds__(256) void conv_splitk_finalize(ConvParams p, int pp
 // the other's MFMAs (v4 is 1 workgroup/CU, 152 KB).  The 8 x 32 tile has 14 % fewer halo rows per
 // output pixel (340 vs 396): 14 % less GroupNorm+SiLU transform VALU and halo traffic.
 
-#ifndef SNRSE_H5_OPAQUE
-#define SNRSE_H5_OPAQUE 0
-#endif
-SNRSE_DEV int h5_opaque(int v) {
-  int r;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
-  return r;
-}
-
 // SCD: the fused 1x1 shortcut's chunks run as LDS-DMA phases interleaved with the main chunks (round 5): a shortcut
 // phase stages its 128 x 32 weights AND its unpadded 256-px x 32-channel input tile (8 + 16 KB = one ring slot) by
 // LDS-DMA, issued at the start of the phase before it like any weight phase, so the tile's HBM latency is covered by
@@ -1601,7 +1576,8 @@ SNRSE_DEV int h5_opaque(int v) {
 // no extra barrier.  (Round 4 ran the shortcut chunks after the main ones as one-tap chunks staged through registers
 // like a halo, whose HBM latency then had one tap of cover each: 3-6 % slower on every shortcut shape, +0.9 % on the
 // C2 line, profiles/r05b_h5_sc_*.)  SCD = the launch has a shortcut; without one the loop is the 3-phase chunk loop.
-template <typename TO, int GNM, int EF, int TW, bool SCD>
+// T: the 16-bit input / weight format (bf16_t or f16_t), TO: the output type
+template <typename T, typename TO, int GNM, int EF, int TW, bool SCD>
 __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   constexpr int TH = 256 / TW, HC = TW + 2;
   constexpr int RW = TH / 4;                // image rows per wave
@@ -1620,13 +1596,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   // thread keeps them in registers across the MFMA phases
   float* const gnl = (float*)(smem + HALO_BYTES + 2 * SLOT + 1024);  // past the stamps build's area
 
-#if SNRSE_H5_OPAQUE
-  // lane-derived values come from an opaque copy of the thread index, so the compiler re-derives
-  // them where they are used instead of keeping them in VGPRs across the whole kernel
-  const int tid = h5_opaque((int)threadIdx.x), lane = tid & 63;
-#else
   const int tid = threadIdx.x, lane = tid & 63;
-#endif
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
 #ifdef SNRSE_STAMPS
   unsigned long long* const lst = (unsigned long long*)(ring + 2 * SLOT) + wid * 32;
@@ -1712,7 +1682,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
       if (j == HJ - 1 && hr >= HROWS) break;
       u32x4 v = hv[j];
       if constexpr (GNM > 0) {
-        if (tr) v = gn_xform8<GNM>(v, gsc, gsh, hok[j]);  // outside the image: the conv's zero padding
+        if (tr) v = gn_xform8<T, GNM>(v, gsc, gsh, hok[j]);  // outside the image: the conv's zero padding
       }
       *(u32x4*)(halo + swz64(hr, hcol)) = v;
     }
@@ -1857,7 +1827,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[h][i][j] = mfma_chunk<bf16_t>(af[i], bfr[h * 4 + j], acc[h][i][j]);
+            for (int j = 0; j < 4; ++j) acc[h][i][j] = mfma_chunk<T>(af[i], bfr[h * 4 + j], acc[h][i][j]);
       }
       if (c + 1 < cbm) {
         if (kind == 2) {
@@ -1925,7 +1895,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            acc[h][i][j] = mfma_chunk<bf16_t>(af[i], bfr[h * 4 + j], acc[h][i][j]);  // D[px][co]
+            acc[h][i][j] = mfma_chunk<T>(af[i], bfr[h * 4 + j], acc[h][i][j]);  // D[px][co]
     }
     SNRSE_STAMP(3 + 2 * (q & 15));
     if (last && c + 1 < cbm) {
@@ -1977,21 +1947,21 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
 #endif
 }
 
-template <typename TO, int GNM, int EF, int TW, bool SCD>
+template <typename T, typename TO, int GNM, int EF, int TW, bool SCD>
 int launch_halo5_ef(ConvParams p, int grid, hipStream_t s) {
   // halo + weight ring + (stamps build: 4 x 32 stamps) + the next chunk's GroupNorm affine (2 x 32 f32),
   // and at least the epilogue's reuse of it: 4 waves' 64 x 68 f32 staging + the 4 x 128 x 2 f32 statistics
   constexpr size_t main_lds = (256 / TW + 2) * (TW + 2) * 64 + 2 * 3 * 128 * 64 + 1024 + 256;
   constexpr size_t epi_lds = 4 * (64 * 68 * 4) + 4 * 128 * 2 * 4;
   constexpr size_t lds = main_lds > epi_lds ? main_lds : epi_lds;
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_halo5_kernel<TO, GNM, EF, TW, SCD>,
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_halo5_kernel<T, TO, GNM, EF, TW, SCD>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   SNRSE_RET(attr);  // (thread-safe one-time set: a function-local static)
-  hipLaunchKernelGGL((conv_halo5_kernel<TO, GNM, EF, TW, SCD>), dim3(grid), dim3(256), lds, s, p);
+  hipLaunchKernelGGL((conv_halo5_kernel<T, TO, GNM, EF, TW, SCD>), dim3(grid), dim3(256), lds, s, p);
   return (int)hipGetLastError();
 }
 
-template <typename TO, int GNM, int TW>
+template <typename T, typename TO, int GNM, int TW>
 int launch_halo5_gn(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   p.ntn = p.Cout / 128;
   // non-temporal output stores when the output exceeds the 256 MB Infinity Cache (+1 % on the
@@ -2002,14 +1972,14 @@ int launch_halo5_gn(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   const int tiles = p.B * (p.H / (256 / TW)) * (p.W / TW) * p.ntn;
   const int grid = tiles;
   const bool scd = p.sc_src != nullptr;  // the fused shortcut's chunks as LDS-DMA phases
-  // the bf16 ResBlock configurations of the NCSN++ path get a branch-free epilogue (bias always on):
+  // the 16-bit ResBlock configurations of the NCSN++ path get a branch-free epilogue (bias always on):
   // Conv_0 (+temb), Conv_1 (+residual | +1x1 shortcut as extra K | +Combine), each +-stats, +-NT
   if constexpr (sizeof(TO) == 2 && GNM != 1) {
     if (cx.h5_specialise && p.bias) {
 #define SNRSE_H5_EF(F) \
-  case (F): return launch_halo5_ef<TO, GNM, (F), TW, false>(p, grid, s);
+  case (F): return launch_halo5_ef<T, TO, GNM, (F), TW, false>(p, grid, s);
 #define SNRSE_H5_EFS(F) \
-  case (F): return launch_halo5_ef<TO, GNM, (F), TW, true>(p, grid, s);
+  case (F): return launch_halo5_ef<T, TO, GNM, (F), TW, true>(p, grid, s);
       if (!scd) {
         switch (epi_flags(p)) {
           SNRSE_H5_EF(EF_TEMB | EF_STATS)
@@ -2033,26 +2003,27 @@ int launch_halo5_gn(ConvParams p, hipStream_t s, snrse_ctx& cx) {
 #undef SNRSE_H5_EFS
     }
   }
-  return scd ? launch_halo5_ef<TO, GNM, EF_RT, TW, true>(p, grid, s) : launch_halo5_ef<TO, GNM, EF_RT, TW, false>(p, grid, s);
+  return scd ? launch_halo5_ef<T, TO, GNM, EF_RT, TW, true>(p, grid, s)
+             : launch_halo5_ef<T, TO, GNM, EF_RT, TW, false>(p, grid, s);
 }
 
 // GroupNorm prologue mode and tile width as template arguments: the halo transform is straight-line
 // code.  Tile 8 x 32 where H % 8 == 0 (option h5_tw: 0 auto, 64 / 32 force where legal), else 4 x 64.
-template <typename TO, int TW>
+template <typename T, typename TO, int TW>
 int launch_halo5_tw(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   cx.last_tw = TW;
-  if (!p.gn_scale) return launch_halo5_gn<TO, 0, TW>(p, s, cx);
-  if (!p.gn_act) return launch_halo5_gn<TO, 1, TW>(p, s, cx);
-  return launch_halo5_gn<TO, 2, TW>(p, s, cx);
+  if (!p.gn_scale) return launch_halo5_gn<T, TO, 0, TW>(p, s, cx);
+  if (!p.gn_act) return launch_halo5_gn<T, TO, 1, TW>(p, s, cx);
+  return launch_halo5_gn<T, TO, 2, TW>(p, s, cx);
 }
 
 inline bool halo_tile32(const ConvParams& p) { return p.H % 8 == 0 && p.W % 32 == 0; }
 inline bool halo_tile64(const ConvParams& p) { return p.H % 4 == 0 && p.W % 64 == 0; }
 
-template <typename TO>
+template <typename T, typename TO>
 int launch_halo5(ConvParams p, hipStream_t s, snrse_ctx& cx) {
-  if (halo_tile32(p) && cx.h5_tw != 64) return launch_halo5_tw<TO, 32>(p, s, cx);
-  return launch_halo5_tw<TO, 64>(p, s, cx);
+  if (halo_tile32(p) && cx.h5_tw != 64) return launch_halo5_tw<T, TO, 32>(p, s, cx);
+  return launch_halo5_tw<T, TO, 64>(p, s, cx);
 }
 
 // K splits for a v2 launch of `tiles` output tiles over nk K-tiles: about one workgroup per CU when
@@ -2171,10 +2142,10 @@ int launch_x3h(const ConvParams& p, hipStream_t s, int tiles, int spread, int tw
   return spread ? launch_x3h_spr<1, 64>(p, s, tiles, spec) : launch_x3h_spr<0, 64>(p, s, tiles, spec);
 }
 
-template <int BM, int BN, typename TO>
+template <int BM, int BN, typename T, typename TO>
 int launch_glds(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   constexpr size_t lds = (size_t)3 * (BM + BN) * 128;
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_glds_kernel<BM, BN, TO>,
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_glds_kernel<BM, BN, T, TO>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   SNRSE_RET(attr);
   p.ntn = p.Cout / BN;
@@ -2183,7 +2154,7 @@ int launch_glds(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   p.ksplit = choose_ksplit(p, ntm * p.ntn, nk, cx);
   p.ws = cx.ws;
   cx.last_ksplit = p.ksplit;
-  hipLaunchKernelGGL((conv_glds_kernel<BM, BN, TO>), dim3(ntm * p.ntn * p.ksplit), dim3(512), lds, s, p);
+  hipLaunchKernelGGL((conv_glds_kernel<BM, BN, T, TO>), dim3(ntm * p.ntn * p.ksplit), dim3(512), lds, s, p);
   if (p.ksplit > 1) {
     SNRSE_LAUNCH_CHECK();
     const int HW = p.H * p.W, ppb = 64;
@@ -2213,12 +2184,12 @@ int dispatch_conv(const ConvParams& p, hipStream_t s, snrse_ctx& cx) {
         // 4 % faster there and +0.4 % on the C2 line, profiles/r05h_*; it was removed -- git history, conv_h10.hip.)
         if (cx.conv_variant != 2 && p.ksize == 3 && halo_tile64(p)) {
           cx.last_kernel = kHaloAuto;
-          return launch_halo5<TO>(p, s, cx);
+          return launch_halo5<T, TO>(p, s, cx);
         }
         if (p.gn_scale) return SNRSE_EINVAL;  // fused GroupNorm exists only on the halo paths
         cx.last_kernel = 2;
-        if (p.Cout % 256 == 0) return launch_glds<128, 256, TO>(p, s, cx);
-        return launch_glds<256, 128, TO>(p, s, cx);
+        if (p.Cout % 256 == 0) return launch_glds<128, 256, T, TO>(p, s, cx);
+        return launch_glds<256, 128, T, TO>(p, s, cx);
       }
     }
     if (p.gn_scale) return SNRSE_EINVAL;
@@ -2232,12 +2203,12 @@ int dispatch_conv(const ConvParams& p, hipStream_t s, snrse_ctx& cx) {
     if (cx.conv_variant != 1 && head_ok(p) && !small) {
       const bool part = cx.head_part != 0 && p.Cout == 4;
       cx.last_kernel = part ? 15 : 10;
-      return launch_head(p, s, part);
+      return launch_head(p, s, part, std::is_same_v<T, f16_t>);
     }
     if (cx.conv_variant != 1 && cx.head_small && head_small_ok(p)) {
       cx.last_kernel = 14;
       cx.last_ksplit = 1;
-      return launch_head_small(p, s);
+      return launch_head_small(p, s, false, std::is_same_v<T, f16_t>);
     }
   }
   if (p.gn_scale) return SNRSE_EINVAL;
@@ -2256,7 +2227,7 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
                             const float* comb_b, void* out, int Cout, int out_ld, double* stats,
                             const float* gn_scale, const float* gn_shift, int gn_act, int dtype,
                             int out_f32, hipStream_t stream) {
-  using TrB = ConvTraits<bf16_t>;
+  using TrB = ConvTraits<bf16_t>;  // (f16: the same 64-element K-tiles)
   using TrF = ConvTraits<float>;
   snrse_ctx& cx = *snrse_ctx_resolve(ctx);
   // SNRSE_F32X3: fp32 activations / output, weights pre-split into bf16 hi / lo rows (conv_x3_kernel)
@@ -2266,7 +2237,7 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
     dtype = SNRSE_F32;
     out_f32 = 0;  // (the output is fp32 anyway)
   }
-  const int KT = dtype == SNRSE_BF16 ? TrB::KT : TrF::KT;
+  const int KT = snrse_is16(dtype) ? TrB::KT : TrF::KT;
   if (!src0 || !wgt || !out || (ksize != 1 && ksize != 3)) return SNRSE_EINVAL;
   if (C0 % KT || C1 % KT || (sc_src && (Csc % KT || Csc1 % KT))) return SNRSE_EINVAL;
   if (sc_src && Csc1 > 0 && !sc_src1) return SNRSE_EINVAL;
@@ -2291,7 +2262,7 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
   p.gn_scale = gn_scale; p.gn_shift = gn_shift; p.gn_act = gn_act;
   if ((gn_scale == nullptr) != (gn_shift == nullptr)) return SNRSE_EINVAL;
   if (p.M <= 0) return 0;
-  const long long esz = dtype == SNRSE_BF16 ? 2 : 4;
+  const long long esz = snrse_is16(dtype) ? 2 : 4;
   const long long pix = (long long)B * H * W;
   p.bytes0 = pix * C0 * esz; p.bytes1 = pix * C1 * esz;
   p.sc_bytes0 = pix * p.Csc * esz; p.sc_bytes1 = pix * p.Csc1 * esz;
@@ -2300,7 +2271,7 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
   p.sc_wbytes = (long long)npad * (p.Csc + p.Csc1) * esz;
   p.ntn = 1;
   if (stats && !cx.stats_zeroed) SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * Cout, stream));
-  if (dtype != SNRSE_BF16 && dtype != SNRSE_F32) return SNRSE_EINVAL;
+  if (!snrse_is16(dtype) && dtype != SNRSE_F32) return SNRSE_EINVAL;
   // the split-bf16 halo-kernel decision is taken once for the whole batch (as ops.x3h_ok takes it, which
   // decides whether the caller passes a GroupNorm prologue), so every image-range chunk of a > 2 GiB call
   // runs the same kernel, however few tiles its last chunk has
@@ -2325,7 +2296,7 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
         return launch_x3h(r, stream, tw32 ? q.B * (q.H / 8) * (q.W / 32) * (q.Cout / 128) : x3h_tiles, cx.x3_spread,
                           tw32 ? 32 : 64, cx.h5_specialise != 0);
       }
-      if (q.Cout <= 16 && cx.conv_variant != 1 && head_ok(q)) {  // the pyramid heads, GroupNorm fused
+      if (q.Cout <= 16 && cx.conv_variant != 1 && head_ok(q, true)) {  // the pyramid heads, GroupNorm fused
         cx.last_kernel = 11;
         cx.last_ksplit = 1;
         return launch_head_x3(q, stream);
@@ -2342,6 +2313,8 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
       if (cx.x3_tile == 3 && q.Cout % 256 == 0) return launch_x3<128, 256, 2, 4>(q, stream, cx);
       return launch_x3<128, 128, 2, 2>(q, stream, cx);
     }
+    if (dtype == SNRSE_F16)
+      return out_f32 ? dispatch_conv<f16_t, float>(q, stream, cx) : dispatch_conv<f16_t, f16_t>(q, stream, cx);
     if (dtype == SNRSE_BF16)
       return out_f32 ? dispatch_conv<bf16_t, float>(q, stream, cx) : dispatch_conv<bf16_t, bf16_t>(q, stream, cx);
     return dispatch_conv<float, float>(q, stream, cx);
@@ -2370,7 +2343,7 @@ extern "C" int snrse_conv2d(snrse_ctx* ctx, const void* src0, int C0, const void
     auto off = [&](const void* ptr, long long elems, long long bytes_per) -> const void* {
       return ptr ? (const void*)((const char*)ptr + elems * bytes_per) : nullptr;
     };
-    const long long osz = (dtype == SNRSE_BF16 && !out_f32) ? 2 : 4;
+    const long long osz = (snrse_is16(dtype) && !out_f32) ? 2 : 4;
     q.src0 = off(p.src0, px0 * C0, esz);
     q.src1 = off(p.src1, px0 * C1, esz);
     q.sc_src = off(p.sc_src, px0 * p.Csc, esz);

@@ -13,6 +13,10 @@ template <> struct ConvTraits<bf16_t> {
   static constexpr int KT = 64;  // elements per K-tile (128 B)
   static constexpr int EPC = 8;  // elements per 16-B chunk
 };
+template <> struct ConvTraits<f16_t> {
+  static constexpr int KT = 64;
+  static constexpr int EPC = 8;
+};
 template <> struct ConvTraits<float> {
   static constexpr int KT = 32;
   static constexpr int EPC = 4;
@@ -71,9 +75,11 @@ SNRSE_DEV f32x4 mfma_chunk(const u32x4& a, const u32x4& b, f32x4 acc);
 
 template <>
 SNRSE_DEV f32x4 mfma_chunk<bf16_t>(const u32x4& a, const u32x4& b, f32x4 acc) {
-  bf16x8_mfma av = __builtin_bit_cast(bf16x8_mfma, a);
-  bf16x8_mfma bv = __builtin_bit_cast(bf16x8_mfma, b);
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+  return H16<bf16_t>::mfma(a, b, acc);
+}
+template <>
+SNRSE_DEV f32x4 mfma_chunk<f16_t>(const u32x4& a, const u32x4& b, f32x4 acc) {
+  return H16<f16_t>::mfma(a, b, acc);
 }
 template <>
 SNRSE_DEV f32x4 mfma_chunk<float>(const u32x4& a, const u32x4& b, f32x4 acc) {
@@ -104,10 +110,11 @@ SNRSE_DEV __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
 }
 
 // Pyramid heads (conv_head.hip): 3x3, Cout <= 16, f32 output, optional fused GroupNorm+SiLU.
-int launch_head(const ConvParams& p, hipStream_t s, bool part = false);
+// f16: the input / weights are IEEE fp16 (else bf16)
+int launch_head(const ConvParams& p, hipStream_t s, bool part, bool f16);
 int launch_head_x3(const ConvParams& p, hipStream_t s);
-bool head_ok(const ConvParams& p);
-int launch_head_small(const ConvParams& p, hipStream_t s, bool split = false);
+bool head_ok(const ConvParams& p, bool x3 = false);
+int launch_head_small(const ConvParams& p, hipStream_t s, bool split = false, bool f16 = false);
 bool head_small_ok(const ConvParams& p);
 
 // Epilogue flags as a compile-time mask (EF >= 0: the halo GEMMs' common configurations, no per-pass
@@ -122,7 +129,8 @@ inline int epi_flags(const ConvParams& p) {  // host side (launch dispatch)
 // ds_read_b128 lane groups for any 16 consecutive rows.
 SNRSE_DEV int swz64(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >> 1) & 3)) << 4); }
 
-// GroupNorm prologue of the halo kernels (v5 GEMM, pyramid head) on one 16-B vector (8 bf16 channels): GNM 1 = affine,
+// GroupNorm prologue of the halo kernels (v5 GEMM, pyramid head) on one 16-B vector (8 channels of the 16-bit format
+// T, out in T): GNM 1 = affine,
 // 2 = affine + SiLU; `ok` = inside the image (else the conv's zero padding).  Written stage by stage
 // over the 8 elements (8 independent exp / rcp chains) so the schedule can hide the transcendental
 // latencies; element by element the chain was fully serial with an s_nop after every exp and rcp.
@@ -133,13 +141,13 @@ SNRSE_DEV int swz64(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >>
 // (fma, exp, fma, rcp, mul) instead of 6.  z -> +inf gives -0 (SiLU's limit), z -> -inf gives y.
 SNRSE_DEV float gn_silu_prescale(float v) { return v * kNegLog2e; }  // (kNegLog2e: common.h)
 
-template <int GNM>
+template <typename T, int GNM>
 SNRSE_DEV u32x4 gn_xform8(const u32x4 v, const float* sc, const float* sh, bool ok) {
   float y[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    y[2 * i] = fmaf(__uint_as_float(v[i] << 16), sc[2 * i], sh[2 * i]);
-    y[2 * i + 1] = fmaf(__uint_as_float(v[i] & 0xffff0000u), sc[2 * i + 1], sh[2 * i + 1]);
+    y[2 * i] = fmaf(H16<T>::lo(v[i]), sc[2 * i], sh[2 * i]);
+    y[2 * i + 1] = fmaf(H16<T>::hi(v[i]), sc[2 * i + 1], sh[2 * i + 1]);
   }
   if constexpr (GNM == 2) {
     // y holds z here.  sched_barrier(0) between the stages: without it the scheduler (at the
@@ -158,7 +166,7 @@ SNRSE_DEV u32x4 gn_xform8(const u32x4 v, const float* sc, const float* sh, bool 
   const uint32_t okm = 0u - (uint32_t)ok;
   u32x4 o;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) o[i] = pack_bf16x2(y[2 * i], y[2 * i + 1]) & okm;
+  for (int i = 0; i < 4; ++i) o[i] = H16<T>::pack(y[2 * i], y[2 * i + 1]) & okm;
   return o;
 }
 

@@ -58,7 +58,7 @@ SNRSE_DEV int kh_swz(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >
 #ifndef SNRSE_HEAD_MINB
 #define SNRSE_HEAD_MINB 1  // workgroups per CU the register allocation is bounded for (A/B builds)
 #endif
-template <int GNM>
+template <typename T, int GNM>
 __global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvParams p) {
   __shared__ __attribute__((aligned(16))) char smem[KH_LDS];
   char* const halo = smem;
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvPar
       const int hr = (tid >> 2) + 64 * j;
       if (j == KH_HJ - 1 && hr >= KH_HROWS) break;
       u32x4 v = h[j];
-      if constexpr (gn) v = gn_xform8<GNM>(v, sc, sh, hok[j]);  // rows outside the image: the conv's zero padding
+      if constexpr (gn) v = gn_xform8<T, GNM>(v, sc, sh, hok[j]);  // rows outside the image: the conv's zero padding
       *(u32x4*)(halo + kh_swz(hr, hcol)) = v;
     }
 #pragma unroll
@@ -162,12 +162,12 @@ __global__ __launch_bounds__(256, SNRSE_HEAD_MINB) void conv_head_kernel(ConvPar
 #pragma unroll
       for (int i = 0; i < 4; ++i) {  // pixels 16 i .. of the wave's 64: row (16 i) / TW, column (16 i) % TW
         const u32x4 bx = *(const u32x4*)(halo + kh_swz(hbase + (16 * i / KH_TW) * KH_HC + (16 * i) % KH_TW, lg));
-        acc[i] = mfma_chunk<bf16_t>(a, bx, acc[i]);
+        acc[i] = mfma_chunk<T>(a, bx, acc[i]);
       }
     }
     __syncthreads();
   };
-  for (int c = 0; c < nc; c += 2) {  // nc is even: bf16 channels come in 64-channel K-tiles (snrse_conv2d)
+  for (int c = 0; c < nc; c += 2) {  // nc is even: 16-bit channels come in 64-channel K-tiles (snrse_conv2d)
     step(c, hv);
     step(c + 1, hw);
   }
@@ -236,7 +236,7 @@ SNRSE_DEV int kp_opaque(int v) {  // a copy the compiler cannot see through: val
 #ifndef SNRSE_HEADP_MINB
 #define SNRSE_HEADP_MINB 3  // three workgroups per CU: <= 168 VGPR + AGPR (the 72 partials accumulators are AGPRs)
 #endif
-template <int GNM>
+template <typename T, int GNM>
 __global__ __launch_bounds__(256, SNRSE_HEADP_MINB) void conv_head_part_kernel(ConvParams p) {
   __shared__ __attribute__((aligned(16))) char smem[KP_LDS];
   char* const halo = smem;
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256, SNRSE_HEADP_MINB) void conv_head_part_kernel(C
       const int hr = (tid >> 2) + 64 * j;
       if (j == KH_HJ - 1 && hr >= KH_HROWS) break;
       u32x4 v = h[j];
-      if constexpr (gn) v = gn_xform8<GNM>(v, sc, sh, hok[j]);  // rows outside the image: the conv's zero padding
+      if constexpr (gn) v = gn_xform8<T, GNM>(v, sc, sh, hok[j]);  // rows outside the image: the conv's zero padding
       *(u32x4*)(halo + kh_swz(hr, hcol)) = v;
     }
     if (tid < 192) *(u32x4*)(wsl + kh_swz(tid >> 2, tid & 3)) = wv;  // 48 columns x 4 16-B chunks
@@ -333,12 +333,12 @@ __global__ __launch_bounds__(256, SNRSE_HEADP_MINB) void conv_head_part_kernel(C
         const u32x4 a = *(const u32x4*)(halo + kh_swz(pb * 16 + lrow, lg));
 #pragma unroll
         for (int cb = 0; cb < 3; ++cb)
-          acc[k][cb] = mfma_chunk<bf16_t>(a, *(const u32x4*)(wsl + kh_swz(cb * 16 + lrow, lg)), acc[k][cb]);
+          acc[k][cb] = mfma_chunk<T>(a, *(const u32x4*)(wsl + kh_swz(cb * 16 + lrow, lg)), acc[k][cb]);
       }
     }
     __syncthreads();
   };
-  for (int c = 0; c < nc; c += 2) {  // nc is even: bf16 channels come in 64-channel K-tiles (snrse_conv2d)
+  for (int c = 0; c < nc; c += 2) {  // nc is even: 16-bit channels come in 64-channel K-tiles (snrse_conv2d)
     step(c, hv);
     step(c + 1, hw);
   }
@@ -541,7 +541,8 @@ constexpr int KS_PX = 8;
 
 // SPLIT (the fp32x3 mode): fp32 input (16-B loads of 4 channels) and weights pre-split per 32-element K-tile into
 // 32 hi then 32 lo bf16 (ops.split_weight); the lane's weights are hi + lo in fp32, so the head is exact fp32 FMAs.
-template <int GNM, bool SPLIT>
+// T: the 16-bit format of the input and weights (bf16 for SPLIT)
+template <typename T, int GNM, bool SPLIT>
 __global__ __launch_bounds__(256) void conv_head_small_kernel(ConvParams p) {
   const int lane = threadIdx.x & 63;
   const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -578,8 +579,7 @@ __global__ __launch_bounds__(256) void conv_head_small_kernel(ConvParams p) {
                     __uint_as_float(h.y & 0xffff0000u) + __uint_as_float(l.y & 0xffff0000u)};
         } else {
           h = *(const uint2*)(wg + (size_t)co * K1 + k);
-          w = f32x4{__uint_as_float(h.x << 16), __uint_as_float(h.x & 0xffff0000u), __uint_as_float(h.y << 16),
-                    __uint_as_float(h.y & 0xffff0000u)};
+          w = f32x4{H16<T>::lo(h.x), H16<T>::hi(h.x), H16<T>::lo(h.y), H16<T>::hi(h.y)};
         }
         wq[tp][co] = w;
       }
@@ -603,8 +603,8 @@ __global__ __launch_bounds__(256) void conv_head_small_kernel(ConvParams p) {
           v[0] = r[0]; v[1] = r[1]; v[2] = r[2]; v[3] = r[3];
         } else {
           const uint2 raw = *(const uint2*)((const bf16_t*)p.src0 + pix * C + c);
-          v[0] = __uint_as_float(raw.x << 16); v[1] = __uint_as_float(raw.x & 0xffff0000u);
-          v[2] = __uint_as_float(raw.y << 16); v[3] = __uint_as_float(raw.y & 0xffff0000u);
+          v[0] = H16<T>::lo(raw.x); v[1] = H16<T>::hi(raw.x);
+          v[2] = H16<T>::lo(raw.y); v[3] = H16<T>::hi(raw.y);
         }
         if constexpr (GNM > 0) {
 #pragma unroll
@@ -653,53 +653,63 @@ bool head_small_ok(const ConvParams& p) {
   return (long long)p.B * p.H * ((p.W + KS_PX - 1) / KS_PX) < 0x7fffffffLL;
 }
 
-// split: the fp32x3 form (fp32 input, split weights)
-int launch_head_small(const ConvParams& p, hipStream_t s, bool split) {
+// split: the fp32x3 form (fp32 input, split weights); f16: fp16 input and weights (else bf16)
+int launch_head_small(const ConvParams& p, hipStream_t s, bool split, bool f16) {
   if (!head_small_ok(p)) return SNRSE_EINVAL;
   const long long waves = (long long)p.B * p.H * ((p.W + KS_PX - 1) / KS_PX);
   const unsigned blocks = (unsigned)((waves + 3) / 4);
-#define SNRSE_HS(G_, S_) hipLaunchKernelGGL((conv_head_small_kernel<G_, S_>), dim3(blocks), dim3(256), 0, s, p)
+#define SNRSE_HS(T_, G_, S_) hipLaunchKernelGGL((conv_head_small_kernel<T_, G_, S_>), dim3(blocks), dim3(256), 0, s, p)
   if (split) {
-    if (!p.gn_scale) SNRSE_HS(0, true);
-    else if (!p.gn_act) SNRSE_HS(1, true);
-    else SNRSE_HS(2, true);
+    if (!p.gn_scale) SNRSE_HS(bf16_t, 0, true);
+    else if (!p.gn_act) SNRSE_HS(bf16_t, 1, true);
+    else SNRSE_HS(bf16_t, 2, true);
+  } else if (f16) {
+    if (!p.gn_scale) SNRSE_HS(f16_t, 0, false);
+    else if (!p.gn_act) SNRSE_HS(f16_t, 1, false);
+    else SNRSE_HS(f16_t, 2, false);
   } else {
-    if (!p.gn_scale) SNRSE_HS(0, false);
-    else if (!p.gn_act) SNRSE_HS(1, false);
-    else SNRSE_HS(2, false);
+    if (!p.gn_scale) SNRSE_HS(bf16_t, 0, false);
+    else if (!p.gn_act) SNRSE_HS(bf16_t, 1, false);
+    else SNRSE_HS(bf16_t, 2, false);
   }
 #undef SNRSE_HS
   return (int)hipGetLastError();
 }
 
-bool head_ok(const ConvParams& p) {
+// x3: the split-bf16 head (conv_head_x3_kernel), which has no LDS GroupNorm table and so no channel cap
+bool head_ok(const ConvParams& p, bool x3) {
   if (p.ksize != 3 || p.Cout > 16 || p.Cout % 4 || p.H % KH_TH || p.W % KH_TW || p.B <= 0) return false;
-  if (p.C0 % 32 || p.C1 % 32 || p.C0 + p.C1 <= 0 || p.C0 + p.C1 > KH_MAXC) return false;
+  if (p.C0 % 32 || p.C1 % 32 || p.C0 + p.C1 <= 0 || (!x3 && p.C0 + p.C1 > KH_MAXC)) return false;
   if (p.sc_src || p.temb || p.comb_src || p.stats) return false;
   if (p.out_ld % 4 || (p.res && p.res_ld % 4)) return false;
   const long long lim = 0x7ff00000ll;
   return p.bytes0 < lim && p.bytes1 < lim && p.wbytes < lim;
 }
 
-int launch_head(const ConvParams& p, hipStream_t s, bool part) {
+template <typename T>
+static int launch_head_t(const ConvParams& p, hipStream_t s, bool part, unsigned tiles) {
+  if (part && p.Cout == 4) {
+    if (!p.gn_scale) hipLaunchKernelGGL((conv_head_part_kernel<T, 0>), dim3(tiles), dim3(256), 0, s, p);
+    else if (!p.gn_act) hipLaunchKernelGGL((conv_head_part_kernel<T, 1>), dim3(tiles), dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((conv_head_part_kernel<T, 2>), dim3(tiles), dim3(256), 0, s, p);
+    return (int)hipGetLastError();
+  }
+  if (!p.gn_scale) hipLaunchKernelGGL((conv_head_kernel<T, 0>), dim3(tiles), dim3(256), 0, s, p);
+  else if (!p.gn_act) hipLaunchKernelGGL((conv_head_kernel<T, 1>), dim3(tiles), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL((conv_head_kernel<T, 2>), dim3(tiles), dim3(256), 0, s, p);
+  return (int)hipGetLastError();
+}
+
+int launch_head(const ConvParams& p, hipStream_t s, bool part, bool f16) {
   if (!head_ok(p)) return SNRSE_EINVAL;
   const long long tiles = (long long)p.B * (p.H / KH_TH) * (p.W / KH_TW);
   if (tiles <= 0 || tiles > 0x7fffffffLL) return SNRSE_EINVAL;
-  if (part && p.Cout == 4) {
-    if (!p.gn_scale) hipLaunchKernelGGL(conv_head_part_kernel<0>, dim3((unsigned)tiles), dim3(256), 0, s, p);
-    else if (!p.gn_act) hipLaunchKernelGGL(conv_head_part_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, s, p);
-    else hipLaunchKernelGGL(conv_head_part_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, s, p);
-    return (int)hipGetLastError();
-  }
-  if (!p.gn_scale) hipLaunchKernelGGL(conv_head_kernel<0>, dim3((unsigned)tiles), dim3(256), 0, s, p);
-  else if (!p.gn_act) hipLaunchKernelGGL(conv_head_kernel<1>, dim3((unsigned)tiles), dim3(256), 0, s, p);
-  else hipLaunchKernelGGL(conv_head_kernel<2>, dim3((unsigned)tiles), dim3(256), 0, s, p);
-  return (int)hipGetLastError();
+  return f16 ? launch_head_t<f16_t>(p, s, part, (unsigned)tiles) : launch_head_t<bf16_t>(p, s, part, (unsigned)tiles);
 }
 
 // the split-bf16 form: same shape contract, fp32 activations (p.bytes* are fp32 extents)
 int launch_head_x3(const ConvParams& p, hipStream_t s) {
-  if (!head_ok(p)) return SNRSE_EINVAL;
+  if (!head_ok(p, true)) return SNRSE_EINVAL;
   const long long tiles = (long long)p.B * (p.H / KH_TH) * (p.W / KH_TW);
   if (tiles <= 0 || tiles > 0x7fffffffLL) return SNRSE_EINVAL;
   if (!p.gn_scale) hipLaunchKernelGGL(conv_head_x3_kernel<0>, dim3((unsigned)tiles), dim3(256), 0, s, p);

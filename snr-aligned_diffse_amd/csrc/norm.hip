@@ -20,17 +20,14 @@ namespace {
 
 template <typename T> struct VecT;
 template <> struct VecT<bf16_t> { static constexpr int N = 8; };
+template <> struct VecT<f16_t> { static constexpr int N = 8; };
 template <> struct VecT<float> { static constexpr int N = 4; };
 
 template <typename T>
 SNRSE_DEV void load_vec(const T* p, float* v) {
   const u32x4 r = *(const u32x4*)p;
   if constexpr (sizeof(T) == 2) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[2 * i] = __uint_as_float(r[i] << 16);
-      v[2 * i + 1] = __uint_as_float(r[i] & 0xffff0000u);
-    }
+    unpack8<T>(r, v);
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = __uint_as_float(r[i]);
@@ -41,8 +38,7 @@ template <typename T>
 SNRSE_DEV void store_vec(T* p, const float* v) {
   u32x4 r;
   if constexpr (sizeof(T) == 2) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = (uint32_t)f2bf(v[2 * i]) | ((uint32_t)f2bf(v[2 * i + 1]) << 16);
+    r = pack8<T>(v);
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) r[i] = __float_as_uint(v[i]);
@@ -156,7 +152,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const Tin* src0, int C0, 
   const int op0 = blockIdx.x * opix_per_blk;
   if constexpr (MODE == MODE_NONE && sizeof(Tout) == sizeof(Tin)) {
     // elementwise: UNR vectors' loads in flight before any is transformed (a load-use chain per vector held
-    // the small-level GroupNorm launches at ~13 us); bf16 takes the fast SiLU as gn_act does, fp32 the exact one
+    // the small-level GroupNorm launches at ~13 us); 16-bit takes the fast SiLU as gn_act does, fp32 the exact one
     constexpr int UNR = 4;
     const int HWo = Ho * Wo;
     const int tot = min(opix_per_blk, HWo - op0) * LP;
@@ -178,11 +174,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const Tin* src0, int C0, 
           const int op = op0 + idx / LP, c = (idx % LP) * V;
           float x[V];
           if constexpr (sizeof(Tin) == 2) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              x[2 * i] = __uint_as_float(raw[u][i] << 16);
-              x[2 * i + 1] = __uint_as_float(raw[u][i] & 0xffff0000u);
-            }
+            unpack8<Tin>(raw[u], x);
           } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i) x[i] = __uint_as_float(raw[u][i]);
@@ -340,7 +332,7 @@ extern "C" int snrse_gn_scale_shift(const double* sums0, int C0, const double* s
 
 extern "C" int snrse_gn_stats(snrse_ctx* ctx, const void* src0, int C0, const void* src1, int C1, int B, int HW,
                               double* sums, double* sums1, int dtype, hipStream_t stream) {
-  const int V = dtype == SNRSE_BF16 ? 8 : 4;
+  const int V = snrse_is16(dtype) ? 8 : 4;
   const int C = C0 + C1;
   if (C % V || C0 % V || C / V > 256 || !sums || (C1 > 0 && !sums1)) return SNRSE_EINVAL;
   const bool zeroed = snrse_ctx_resolve(ctx)->stats_zeroed != 0;
@@ -351,7 +343,10 @@ extern "C" int snrse_gn_stats(snrse_ctx* ctx, const void* src0, int C0, const vo
   const int ppb = (HW + nblk - 1) / nblk;
   dim3 grid(nblk, B);
   const size_t lds = sizeof(float) * 2 * C;
-  if (dtype == SNRSE_BF16)
+  if (dtype == SNRSE_F16)
+    hipLaunchKernelGGL(gn_stats_kernel<f16_t>, grid, dim3(256), lds, stream, (const f16_t*)src0, C0,
+                       (const f16_t*)src1, C1, HW, ppb, sums, sums1);
+  else if (dtype == SNRSE_BF16)
     hipLaunchKernelGGL(gn_stats_kernel<bf16_t>, grid, dim3(256), lds, stream, (const bf16_t*)src0, C0,
                        (const bf16_t*)src1, C1, HW, ppb, sums, sums1);
   else if (dtype == SNRSE_F32)
@@ -395,10 +390,13 @@ extern "C" int snrse_gn_apply(const void* src0, int C0, const void* src1, int C1
                               const double* sums, const double* sums1, const float* gamma, const float* beta,
                               int groups,
                               float eps, int act, int mode, void* out, int dtype, hipStream_t stream) {
-  const int V = dtype == SNRSE_BF16 ? 8 : 4;
+  const int V = snrse_is16(dtype) ? 8 : 4;
   if ((C0 + C1) % V || C0 % V) return SNRSE_EINVAL;
   if (sums && (!gamma || !beta || groups <= 0 || (C0 + C1) % groups || (C1 > 0 && !sums1))) return SNRSE_EINVAL;
   if (mode == MODE_DOWN && ((H & 1) || (W & 1))) return SNRSE_EINVAL;
+  if (dtype == SNRSE_F16)
+    return launch_apply<f16_t, f16_t>(src0, C0, src1, C1, B, H, W, sums, sums1, gamma, beta, groups, eps, act,
+                                      mode, out, stream);
   if (dtype == SNRSE_BF16)
     return launch_apply<bf16_t, bf16_t>(src0, C0, src1, C1, B, H, W, sums, sums1, gamma, beta, groups, eps, act,
                                         mode, out, stream);

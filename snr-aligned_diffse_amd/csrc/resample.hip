@@ -39,21 +39,6 @@ template <> struct RTile<MODE_UP> {
   SNRSE_DEV static int in0(int o0) { return o0 / 2 - 1; }
 };
 
-SNRSE_DEV void unpack8(const u32x4 r, float* v) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[2 * i] = __uint_as_float(r[i] << 16);
-    v[2 * i + 1] = __uint_as_float(r[i] & 0xffff0000u);
-  }
-}
-
-SNRSE_DEV u32x4 pack8(const float* v) {
-  u32x4 r;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) r[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
-  return r;
-}
-
 // Linear block id -> XCD-contiguous logical id: consecutive workgroups are dealt round-robin over
 // the 8 XCDs, so without the remap the channel groups of one pixel tile (which share every
 // 128-byte line of the input) would be fetched by 8 different L2s.
@@ -63,19 +48,20 @@ SNRSE_DEV int xcd_logical(int i, int n) {
 }
 
 // grid: B * tiles_y * tiles_x * (C / 16) blocks of 256.  scale/shift [B][C] f32 or null (identity).
-template <int MODE>
-__global__ __launch_bounds__(256) void gn_resample_kernel(const bf16_t* __restrict__ src, int C, int H, int W,
+// E: the 16-bit format (bf16_t / f16_t)
+template <typename E, int MODE>
+__global__ __launch_bounds__(256) void gn_resample_kernel(const E* __restrict__ src, int C, int H, int W,
                                                           int tiles_x, int tiles_y, const float* __restrict__ scale,
                                                           const float* __restrict__ shift, int act,
-                                                          bf16_t* __restrict__ out_act, bf16_t* __restrict__ out_raw) {
+                                                          E* __restrict__ out_act, E* __restrict__ out_raw) {
   using T = RTile<MODE>;
   constexpr int NPX = T::ITY * T::ITX;
   // down: the activated tile is kept as bf16 (2 x 19.6 KB instead of 39 + 19.6 KB, so 4 blocks
   // share a CU: level-0 759 -> 501 us); up (17 KB tile, 4 taps per output) keeps f32, where the
   // extra unpacking cost more than the occupancy gained
-  using ActT = std::conditional_t<MODE == MODE_DOWN, bf16_t, float>;
+  using ActT = std::conditional_t<MODE == MODE_DOWN, E, float>;
   __shared__ __attribute__((aligned(16))) ActT s_act[NPX * kCB];
-  __shared__ __attribute__((aligned(16))) bf16_t s_raw[NPX * kCB];
+  __shared__ __attribute__((aligned(16))) E s_raw[NPX * kCB];
   const int ncg = C / kCB;
   int id = xcd_logical(blockIdx.x, gridDim.x);
   const int cg = id % ncg;
@@ -130,7 +116,7 @@ __global__ __launch_bounds__(256) void gn_resample_kernel(const bf16_t* __restri
     if (idx >= NPX * kNV) break;
     const int p = idx / kNV;
     float x[8], a[8];
-    unpack8(rv[k], x);
+    unpack8<E>(rv[k], x);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float y = fmaf(x[i], sc[i], sh[i]);
@@ -138,7 +124,7 @@ __global__ __launch_bounds__(256) void gn_resample_kernel(const bf16_t* __restri
     }
     *(u32x4*)(s_raw + p * kCB + 8 * v) = rv[k];
     if constexpr (MODE == MODE_DOWN) {
-      *(u32x4*)(s_act + p * kCB + 8 * v) = pack8(a);
+      *(u32x4*)(s_act + p * kCB + 8 * v) = pack8<E>(a);
     } else {
       f32x4* d = (f32x4*)(s_act + p * kCB + 8 * v);
       d[0] = f32x4{a[0], a[1], a[2], a[3]};
@@ -163,13 +149,13 @@ __global__ __launch_bounds__(256) void gn_resample_kernel(const bf16_t* __restri
       const int q = (py * T::ITX + px) * kCB + 8 * v;
       float x[8], ac[8];
       if constexpr (MODE == MODE_DOWN) {
-        unpack8(*(const u32x4*)(s_act + q), ac);
+        unpack8<E>(*(const u32x4*)(s_act + q), ac);
       } else {
         const f32x4 a0 = *(const f32x4*)(s_act + q), a1 = *(const f32x4*)(s_act + q + 4);
 #pragma unroll
         for (int i = 0; i < 4; ++i) { ac[i] = a0[i]; ac[i + 4] = a1[i]; }
       }
-      unpack8(*(const u32x4*)(s_raw + q), x);
+      unpack8<E>(*(const u32x4*)(s_raw + q), x);
 #pragma unroll
       for (int i = 0; i < 8; ++i) oa[i] = fmaf(ac[i], w, oa[i]);
 #pragma unroll
@@ -191,8 +177,8 @@ __global__ __launch_bounds__(256) void gn_resample_kernel(const bf16_t* __restri
       tap(y0 + 1, x0 + 1, (1.f - wy0) * (1.f - wx0));
     }
     const size_t o = (((size_t)b * Ho + oy) * Wo + ox) * C + c0 + 8 * v;
-    *(u32x4*)(out_act + o) = pack8(oa);
-    if (out_raw) *(u32x4*)(out_raw + o) = pack8(orw);
+    *(u32x4*)(out_act + o) = pack8<E>(oa);
+    if (out_raw) *(u32x4*)(out_raw + o) = pack8<E>(orw);
   }
 }
 
@@ -227,13 +213,13 @@ __global__ __launch_bounds__(256) void gn_act_kernel(const T* __restrict__ src0,
     u32x4 o;
     if constexpr (sizeof(T) == 2) {
       float x[8];
-      unpack8(raw, x);
+      unpack8<T>(raw, x);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float y = fmaf(x[i], s_ss[c + i], s_ss[C + c + i]);
         x[i] = act ? silu(y) : y;
       }
-      o = pack8(x);
+      o = pack8<T>(x);
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -263,24 +249,28 @@ __global__ __launch_bounds__(256) void gn_act_kernel(const T* __restrict__ src0,
 
 // CPT channels of one pixel: bf16 16 B (8 ch) or 8 B (4 ch); f32 16 B (4 ch)
 template <typename E, int CPT> struct RVec;
-template <> struct RVec<bf16_t, 8> {
+template <typename H> struct RVec16_8 {  // 16-bit formats (bf16_t / f16_t), 8 channels
   typedef u32x4 T;
   SNRSE_DEV static T load(__amdgpu_buffer_rsrc_t r, int off) { return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0); }
-  SNRSE_DEV static void unpack(const T v, float* x) { unpack8(v, x); }
-  SNRSE_DEV static T pack(const float* x) { return pack8(x); }
+  SNRSE_DEV static void unpack(const T v, float* x) { unpack8<H>(v, x); }
+  SNRSE_DEV static T pack(const float* x) { return pack8<H>(x); }
 };
-template <> struct RVec<bf16_t, 4> {
+template <typename H> struct RVec16_4 {  // 16-bit formats, 4 channels
   typedef __attribute__((ext_vector_type(2))) unsigned int T;
   SNRSE_DEV static T load(__amdgpu_buffer_rsrc_t r, int off) { return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0); }
   SNRSE_DEV static void unpack(const T v, float* x) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      x[2 * i] = __uint_as_float(v[i] << 16);
-      x[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+      x[2 * i] = H16<H>::lo(v[i]);
+      x[2 * i + 1] = H16<H>::hi(v[i]);
     }
   }
-  SNRSE_DEV static T pack(const float* x) { return T{pack_bf16x2(x[0], x[1]), pack_bf16x2(x[2], x[3])}; }
+  SNRSE_DEV static T pack(const float* x) { return T{H16<H>::pack(x[0], x[1]), H16<H>::pack(x[2], x[3])}; }
 };
+template <> struct RVec<bf16_t, 8> : RVec16_8<bf16_t> {};
+template <> struct RVec<f16_t, 8> : RVec16_8<f16_t> {};
+template <> struct RVec<bf16_t, 4> : RVec16_4<bf16_t> {};
+template <> struct RVec<f16_t, 4> : RVec16_4<f16_t> {};
 template <> struct RVec<float, 4> {
   typedef u32x4 T;
   SNRSE_DEV static T load(__amdgpu_buffer_rsrc_t r, int off) { return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0); }
@@ -580,8 +570,10 @@ int launch_resample(const void* src, int C, int B, int H, int W, const float* sc
     const int r = dispatch_rows<float, MODE>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx);
     return r >= 0 ? r : SNRSE_EINVAL;
   }
+  const bool f16 = dtype == SNRSE_F16;
   if (cx.resample_variant == 0) {
-    const int r = dispatch_rows<bf16_t, MODE>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx);
+    const int r = f16 ? dispatch_rows<f16_t, MODE>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx)
+                      : dispatch_rows<bf16_t, MODE>(src, C, B, H, W, scale, shift, act, out_act, out_raw, stream, cx);
     if (r >= 0) return r;
   }
   if (C % kCB) return SNRSE_EINVAL;
@@ -590,8 +582,12 @@ int launch_resample(const void* src, int C, int B, int H, int W, const float* sc
   const int tiles_y = (Ho + T::OTY - 1) / T::OTY, tiles_x = (Wo + T::OTX - 1) / T::OTX;
   const long long n = (long long)B * tiles_y * tiles_x * (C / kCB);
   if (n <= 0 || n > 0x7fffffffLL) return SNRSE_EINVAL;
-  hipLaunchKernelGGL(gn_resample_kernel<MODE>, dim3((unsigned)n), dim3(256), 0, stream, (const bf16_t*)src, C, H,
-                     W, tiles_x, tiles_y, scale, shift, act, (bf16_t*)out_act, (bf16_t*)out_raw);
+  if (f16)
+    hipLaunchKernelGGL((gn_resample_kernel<f16_t, MODE>), dim3((unsigned)n), dim3(256), 0, stream, (const f16_t*)src, C,
+                       H, W, tiles_x, tiles_y, scale, shift, act, (f16_t*)out_act, (f16_t*)out_raw);
+  else
+    hipLaunchKernelGGL((gn_resample_kernel<bf16_t, MODE>), dim3((unsigned)n), dim3(256), 0, stream, (const bf16_t*)src,
+                       C, H, W, tiles_x, tiles_y, scale, shift, act, (bf16_t*)out_act, (bf16_t*)out_raw);
   return (int)hipGetLastError();
 }
 
@@ -601,7 +597,7 @@ extern "C" int snrse_gn_resample(snrse_ctx* ctx, const void* src, int C, int B, 
                                  const float* shift, int act, int mode, void* out_act, void* out_raw, int dtype,
                                  hipStream_t stream) {
   if (!src || !out_act || C <= 0 || C % (dtype == SNRSE_F32 ? 4 : 8) || B <= 0 || H <= 0 || W <= 0 ||
-      (!scale) != (!shift) || (dtype != SNRSE_BF16 && dtype != SNRSE_F32))
+      (!scale) != (!shift) || (!snrse_is16(dtype) && dtype != SNRSE_F32))
     return SNRSE_EINVAL;
   const snrse_ctx& cx = *snrse_ctx_resolve(ctx);
   if (mode == MODE_DOWN) {
@@ -616,8 +612,8 @@ extern "C" int snrse_gn_resample(snrse_ctx* ctx, const void* src, int C, int B, 
 extern "C" int snrse_gn_act(const void* src0, int C0, const void* src1, int C1, int B, int HW, const float* scale,
                             const float* shift, int act, void* out, int dtype, hipStream_t stream) {
   const int C = C0 + C1;
-  if (dtype != SNRSE_BF16 && dtype != SNRSE_F32) return SNRSE_EINVAL;
-  const int V = dtype == SNRSE_BF16 ? 8 : 4;
+  if (!snrse_is16(dtype) && dtype != SNRSE_F32) return SNRSE_EINVAL;
+  const int V = snrse_is16(dtype) ? 8 : 4;
   if (!src0 || !out || C0 <= 0 || C0 % V || C1 < 0 || C1 % V || (C1 > 0 && !src1) || B <= 0 || HW <= 0 ||
       (!scale) != (!shift) || C > 4096)
     return SNRSE_EINVAL;
@@ -625,7 +621,10 @@ extern "C" int snrse_gn_act(const void* src0, int C0, const void* src1, int C1, 
   int ppb = (8 * 256) / LP;  // ~8 vectors per thread
   if (ppb < 1) ppb = 1;
   dim3 grid((HW + ppb - 1) / ppb, B);
-  if (dtype == SNRSE_BF16)
+  if (dtype == SNRSE_F16)
+    hipLaunchKernelGGL(gn_act_kernel<f16_t>, grid, dim3(256), sizeof(float) * 2 * C, stream, (const f16_t*)src0, C0,
+                       (const f16_t*)src1, C1, HW, ppb, scale, shift, act, (f16_t*)out);
+  else if (dtype == SNRSE_BF16)
     hipLaunchKernelGGL(gn_act_kernel<bf16_t>, grid, dim3(256), sizeof(float) * 2 * C, stream, (const bf16_t*)src0, C0,
                        (const bf16_t*)src1, C1, HW, ppb, scale, shift, act, (bf16_t*)out);
   else

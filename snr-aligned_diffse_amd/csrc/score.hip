@@ -216,8 +216,7 @@ __global__ __launch_bounds__(256) void input_pack_kernel(const float2* x, const 
   }
   u32x4 o;
   if constexpr (sizeof(T) == 2) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
+    o = pack8<T>(v);
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[i] = __float_as_uint(v[i]);
@@ -225,7 +224,7 @@ __global__ __launch_bounds__(256) void input_pack_kernel(const float2* x, const 
   *(u32x4*)(col + (size_t)p * 64 + k * VEC) = o;
 }
 
-// ---- fused input conv (bf16): complex (x, y) -> h = conv3x3(4 -> 128) + bias, NHWC bf16 -------
+// ---- fused input conv (16-bit T): complex (x, y) -> h = conv3x3(4 -> 128) + bias, NHWC T -------
 // (ncsnpp.py:253-254, 282-285).  Replaces input_pack's 64-channel im2col round trip through HBM +
 // a K=64 GEMM: the 36 products per output come from x / y directly (cache-resident neighbours),
 // so the launch is bound by the 256 B/pixel output store.  MFMA 16x16x32 with A = the packed
@@ -257,9 +256,10 @@ SNRSE_DEV float ic_row_sum16(float v) {
   return v;
 }
 
+template <typename T>
 __global__ __launch_bounds__(256) void input_conv_kernel(const float2* __restrict__ x, const float2* __restrict__ y,
-                                                         int H, int W, const bf16_t* __restrict__ wgt,
-                                                         const float* __restrict__ bias, bf16_t* __restrict__ out,
+                                                         int H, int W, const T* __restrict__ wgt,
+                                                         const float* __restrict__ bias, T* __restrict__ out,
                                                          float* __restrict__ pyr, double* __restrict__ stats) {
   __shared__ float s_st[4][128 * 2];  // per-wave channel sums: fixed-order fold, no LDS atomics
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -327,8 +327,8 @@ __global__ __launch_bounds__(256) void input_conv_kernel(const float2* __restric
       const float2 a = cok[u] ? cx[u] : make_float2(0.f, 0.f);
       const float2 c = cok[u] ? cy[u] : make_float2(0.f, 0.f);
       const int sl = u < 2 ? 0 : 1, hw_ = u < 2 ? 2 * u : 0;
-      pf[sl][hw_] = pack_bf16x2(a.x, a.y);
-      pf[sl][hw_ + 1] = pack_bf16x2(c.x, c.y);
+      pf[sl][hw_] = H16<T>::pack(a.x, a.y);
+      pf[sl][hw_ + 1] = H16<T>::pack(c.x, c.y);
     }
     pf[1][2] = 0u;
     pf[1][3] = 0u;
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256) void input_conv_kernel(const float2* __restric
       *(float4*)(pyr + (img + (size_t)h * W + w) * 4) = make_float4(cx[0].x, cx[0].y, cy[0].x, cy[0].y);
     // channel blocks (2jp, 2jp + 1) are exchanged between DPP rows (v_permlane16_swap) so each lane
     // stores 8 consecutive channels: 16-B stores, 64 contiguous bytes of a pixel per instruction
-    bf16_t* orow = out + (img + (size_t)h * W + w) * 128 + 8 * (g >> 1);
+    T* orow = out + (img + (size_t)h * W + w) * 128 + 8 * (g >> 1);
 #pragma unroll
     for (int jp = 0; jp < 4; ++jp) {
       uint32_t pk[2][2];
@@ -344,8 +344,8 @@ __global__ __launch_bounds__(256) void input_conv_kernel(const float2* __restric
       for (int hh = 0; hh < 2; ++hh) {
         const int j = 2 * jp + hh;
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        acc = mfma_bf16_16x16x32(wf[j][0], pf[0], acc);
-        acc = mfma_bf16_16x16x32(wf[j][1], pf[1], acc);
+        acc = H16<T>::mfma(wf[j][0], pf[0], acc);
+        acc = H16<T>::mfma(wf[j][1], pf[1], acc);
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -353,8 +353,8 @@ __global__ __launch_bounds__(256) void input_conv_kernel(const float2* __restric
           s1[j][e] += v[e];
           s2[j][e] = fmaf(v[e], v[e], s2[j][e]);
         }
-        pk[hh][0] = pack_bf16x2(v[0], v[1]);
-        pk[hh][1] = pack_bf16x2(v[2], v[3]);
+        pk[hh][0] = H16<T>::pack(v[0], v[1]);
+        pk[hh][1] = H16<T>::pack(v[2], v[3]);
       }
       const auto r0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
       const auto r1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
@@ -397,10 +397,10 @@ __global__ __launch_bounds__(256) void input_conv_kernel(const float2* __restric
 // SST (ICH 128): the block's 16 px x 128 ch output (4 KB, contiguous in NHWC) goes through a per-wave LDS stage
 // (16-B chunk c of pixel p at p * 256 + (c ^ (p & 15)) * 16: conflict-free 8-B writes and 16-B reads) and out as 4
 // fully contiguous 1-KB wave stores, instead of 4 stores of 64-B pieces of 16 pixels each
-template <int ICH, bool SST = false>
+template <typename T, int ICH, bool SST = false>
 __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __restrict__ x, const float2* __restrict__ y,
-                                                             int H, int W, const bf16_t* __restrict__ wgt,
-                                                             const float* __restrict__ bias, bf16_t* __restrict__ out,
+                                                             int H, int W, const T* __restrict__ wgt,
+                                                             const float* __restrict__ bias, T* __restrict__ out,
                                                              float* __restrict__ pyr, double* __restrict__ stats) {
   constexpr int NJ = ICH / 16, NS = 128 / ICH;  // channel blocks per wave; waves per pixel stream
   constexpr int TPS = 16 / (4 / NS);            // tiles per pixel stream (4 with ICH 128, 8 with 64)
@@ -473,14 +473,14 @@ __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __res
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
       const int sl = u < 2 ? 0 : 1, hw_ = u < 2 ? 2 * u : 0;
-      pf[sl][hw_] = pack_bf16x2(v[u].x, v[u].y);
-      pf[sl][hw_ + 1] = pack_bf16x2(v[u].z, v[u].w);
+      pf[sl][hw_] = H16<T>::pack(v[u].x, v[u].y);
+      pf[sl][hw_ + 1] = H16<T>::pack(v[u].z, v[u].w);
     }
     pf[1][2] = 0u;
     pf[1][3] = 0u;
     if (g == 2 && jb == 0)  // tap 4 = the pixel itself: the input pyramid (written by one wave of the stream)
       *(float4*)(pyr + (img + (size_t)h * W + w) * 4) = v[0];
-    bf16_t* orow = out + (img + (size_t)h * W + w) * 128 + 8 * (g >> 1);
+    T* orow = out + (img + (size_t)h * W + w) * 128 + 8 * (g >> 1);
     typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 #pragma unroll
     for (int jp = 0; jp < NJ / 2; ++jp) {
@@ -489,8 +489,8 @@ __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __res
       for (int hh = 0; hh < 2; ++hh) {
         const int j = 2 * jp + hh;
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        acc = mfma_bf16_16x16x32(wf[j][0], pf[0], acc);
-        acc = mfma_bf16_16x16x32(wf[j][1], pf[1], acc);
+        acc = H16<T>::mfma(wf[j][0], pf[0], acc);
+        acc = H16<T>::mfma(wf[j][1], pf[1], acc);
         float vv[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -498,8 +498,8 @@ __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __res
           s1[j][e] += vv[e];
           s2[j][e] = fmaf(vv[e], vv[e], s2[j][e]);
         }
-        pk[hh][0] = pack_bf16x2(vv[0], vv[1]);
-        pk[hh][1] = pack_bf16x2(vv[2], vv[3]);
+        pk[hh][0] = H16<T>::pack(vv[0], vv[1]);
+        pk[hh][1] = H16<T>::pack(vv[2], vv[3]);
         if constexpr (SST)  // channels 16 j + 4 g .. + 3 of pixel lr: half (g & 1) of 16-B chunk 2 j + (g >> 1)
           *(u32x2*)(ostg + lr * 256 + (((2 * j + (g >> 1)) ^ lr) << 4) + (g & 1) * 8) = u32x2{pk[hh][0], pk[hh][1]};
       }
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(256) void input_conv_lds_kernel(const float2* __res
     }
     if constexpr (SST) {  // the block's 4 KB: pixel 4 k + (lane >> 4), 16-B chunk lane & 15, contiguous per wave store
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      bf16_t* ob = out + (img + (size_t)h * W + (w - lr)) * 128;
+      T* ob = out + (img + (size_t)h * W + (w - lr)) * 128;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int pp = 4 * k + (lane >> 4), c = lane & 15;
@@ -804,11 +804,9 @@ extern "C" int snrse_temb_dense(const float* temb, const float* W, const float* 
   return launch_dense<1, 0>(temb, nullptr, nullptr, W, bias, out, B, R, D, s);
 }
 
-extern "C" int snrse_input_conv(snrse_ctx* ctx, const void* x, const void* y, int B, int H, int W, const void* wgt, const float* bias,
-                                void* out, float* pyr, double* stats, hipStream_t s) {
-  if (B <= 0 || H <= 0 || W <= 0 || W % 64 || ((long long)H * W / 64) % 16 || !x || !y || !wgt || !bias || !out ||
-      !pyr || !stats)
-    return SNRSE_EINVAL;
+template <typename T>
+static int launch_input_conv(snrse_ctx* ctx, const void* x, const void* y, int B, int H, int W, const void* wgt,
+                             const float* bias, void* out, float* pyr, double* stats, hipStream_t s) {
   if (!snrse_ctx_resolve(ctx)->stats_zeroed)
     SNRSE_RET(hipMemsetAsync(stats, 0, sizeof(double) * 2 * SNRSE_STAT_SLOTS * (size_t)B * 128, s));
   const long long blocks = (long long)B * H * W / (64 * 16);
@@ -816,29 +814,39 @@ extern "C" int snrse_input_conv(snrse_ctx* ctx, const void* x, const void* y, in
   const int lds_rows = 1023 / W + 4;  // (a 1024-px range can touch 1023 / W + 2 rows when W does not divide 1024)
   if (W <= 1024 && snrse_ctx_resolve(ctx)->ic_lds) {
     const size_t lds = (size_t)lds_rows * W * 16;
-    static const hipError_t attr1 = hipFuncSetAttribute((const void*)input_conv_lds_kernel<128>,
+    static const hipError_t attr1 = hipFuncSetAttribute((const void*)input_conv_lds_kernel<T, 128>,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
-    static const hipError_t attr2 = hipFuncSetAttribute((const void*)input_conv_lds_kernel<64>,
+    static const hipError_t attr2 = hipFuncSetAttribute((const void*)input_conv_lds_kernel<T, 64>,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
     SNRSE_RET(attr1);
     SNRSE_RET(attr2);
-    static const hipError_t attr3 = hipFuncSetAttribute((const void*)input_conv_lds_kernel<128, true>,
+    static const hipError_t attr3 = hipFuncSetAttribute((const void*)input_conv_lds_kernel<T, 128, true>,
                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
     SNRSE_RET(attr3);
     if (snrse_ctx_resolve(ctx)->ic_lds == 3)
-      hipLaunchKernelGGL((input_conv_lds_kernel<128, true>), dim3((unsigned)blocks), dim3(256), lds + 4 * 4096, s,
-                         (const float2*)x, (const float2*)y, H, W, (const bf16_t*)wgt, bias, (bf16_t*)out, pyr, stats);
+      hipLaunchKernelGGL((input_conv_lds_kernel<T, 128, true>), dim3((unsigned)blocks), dim3(256), lds + 4 * 4096, s,
+                         (const float2*)x, (const float2*)y, H, W, (const T*)wgt, bias, (T*)out, pyr, stats);
     else if (snrse_ctx_resolve(ctx)->ic_lds == 2)
-      hipLaunchKernelGGL(input_conv_lds_kernel<64>, dim3((unsigned)blocks), dim3(256), lds, s, (const float2*)x,
-                         (const float2*)y, H, W, (const bf16_t*)wgt, bias, (bf16_t*)out, pyr, stats);
+      hipLaunchKernelGGL((input_conv_lds_kernel<T, 64>), dim3((unsigned)blocks), dim3(256), lds, s, (const float2*)x,
+                         (const float2*)y, H, W, (const T*)wgt, bias, (T*)out, pyr, stats);
     else
-      hipLaunchKernelGGL(input_conv_lds_kernel<128>, dim3((unsigned)blocks), dim3(256), lds, s, (const float2*)x,
-                         (const float2*)y, H, W, (const bf16_t*)wgt, bias, (bf16_t*)out, pyr, stats);
+      hipLaunchKernelGGL((input_conv_lds_kernel<T, 128>), dim3((unsigned)blocks), dim3(256), lds, s, (const float2*)x,
+                         (const float2*)y, H, W, (const T*)wgt, bias, (T*)out, pyr, stats);
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL(input_conv_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const float2*)x, (const float2*)y,
-                     H, W, (const bf16_t*)wgt, bias, (bf16_t*)out, pyr, stats);
+  hipLaunchKernelGGL(input_conv_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, s, (const float2*)x, (const float2*)y,
+                     H, W, (const T*)wgt, bias, (T*)out, pyr, stats);
   return (int)hipGetLastError();
+}
+
+// dtype: SNRSE_BF16 or SNRSE_F16 (the format of wgt and out)
+extern "C" int snrse_input_conv(snrse_ctx* ctx, const void* x, const void* y, int B, int H, int W, const void* wgt, const float* bias,
+                                void* out, float* pyr, double* stats, int dtype, hipStream_t s) {
+  if (B <= 0 || H <= 0 || W <= 0 || W % 64 || ((long long)H * W / 64) % 16 || !x || !y || !wgt || !bias || !out ||
+      !pyr || !stats || !snrse_is16(dtype))
+    return SNRSE_EINVAL;
+  return dtype == SNRSE_F16 ? launch_input_conv<f16_t>(ctx, x, y, B, H, W, wgt, bias, out, pyr, stats, s)
+                            : launch_input_conv<bf16_t>(ctx, x, y, B, H, W, wgt, bias, out, pyr, stats, s);
 }
 
 extern "C" int snrse_input_conv_x3(snrse_ctx* ctx, const void* x, const void* y, int B, int H, int W, const void* wgt,
@@ -862,9 +870,12 @@ extern "C" int snrse_input_pack(const void* x, const void* y, int B, int H, int 
                                 int dtype, hipStream_t s) {
   const int total = B * H * W;
   if (total <= 0) return SNRSE_EINVAL;
-  const long long lanes = (long long)total * (dtype == SNRSE_BF16 ? 8 : 16);
+  const long long lanes = (long long)total * (snrse_is16(dtype) ? 8 : 16);
   dim3 grid((unsigned)((lanes + 255) / 256));
-  if (dtype == SNRSE_BF16)
+  if (dtype == SNRSE_F16)
+    hipLaunchKernelGGL(input_pack_kernel<f16_t>, grid, dim3(256), 0, s, (const float2*)x, (const float2*)y, H, W,
+                       (f16_t*)col, pyr, total);
+  else if (dtype == SNRSE_BF16)
     hipLaunchKernelGGL(input_pack_kernel<bf16_t>, grid, dim3(256), 0, s, (const float2*)x, (const float2*)y, H, W,
                        (bf16_t*)col, pyr, total);
   else if (dtype == SNRSE_F32)

@@ -119,7 +119,8 @@ class NCSNpp(nn.Module):
         """The packed device executor for the current parameters (re-packed on change)."""
         key = self._param_key()
         if self._hip_net is None or self._hip_key != key:
-            dt = torch.bfloat16 if self.compute_dtype in ("bf16", torch.bfloat16) else torch.float32
+            dt = {"bf16": torch.bfloat16, torch.bfloat16: torch.bfloat16, "fp16": torch.float16,
+                  torch.float16: torch.float16}.get(self.compute_dtype, torch.float32)
             gemm = "x3" if self.compute_dtype == "fp32x3" else "exact"  # split-bf16 fp32 GEMMs
             dev = device or (torch.device("cuda", torch.cuda.current_device()))
             self._hip_net = _hip.NCSNppHIP(self.state_dict(), dtype=dt, device=dev, gemm=gemm, **self.cfg)

@@ -41,7 +41,7 @@ SIGNATURES = {
     "snrse_stft": [_vp, _i, _i, _vp, _f, _i, _i, _vp, _vp],
     "snrse_absmax": [_vp, _i, _i, _vp, _vp],
     "snrse_energy_ratios": [_vp, _vp, _vp, _i, _i, _vp, _vp],
-    "snrse_input_conv": [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "snrse_input_conv": [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp],
     "snrse_input_conv_x3": [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
     "snrse_spec_transform": [_vp, _vp, C.c_longlong, _i, _vp],
     "snrse_snrnet": [_vp, _i, _i] + [_vp] * 17 + [_vp, _vp, _vp],

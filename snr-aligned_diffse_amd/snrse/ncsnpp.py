@@ -1,4 +1,4 @@
-"""NCSN++ score network executed on the HIP kernels (NHWC, bf16 or exact-fp32 mode).
+"""NCSN++ score network executed on the HIP kernels (NHWC; 16-bit -- fp16 by default, or bf16 -- or the fp32 modes).
 
 Mirrors NCSNpp (reference sgmse/backbones/ncsnpp.py:36-404) for its shipped configuration:
 nf=128, ch_mult=(1,1,2,2,2,2,2), num_res_blocks=2, attn_resolutions=(16,), BigGAN
@@ -23,7 +23,7 @@ import torch
 from . import ops
 
 INV_SQRT2 = 1.0 / math.sqrt(2.0)
-# tests flip this to compare the fused bf16 input conv with the im2col + GEMM path
+# tests flip this to compare the fused 16-bit input conv with the im2col + GEMM path
 _NO_FUSED_INPUT = False
 
 
@@ -115,8 +115,10 @@ def _pack1x1(w, dt, npad=None):
 class NCSNppHIP:
     """Device-resident packed weights + the forward executor."""
 
-    def __init__(self, sd: dict, dtype=torch.bfloat16, device="cuda", gemm="exact", **cfg):
-        """gemm (fp32 only): "exact" = v_mfma_f32_16x16x4_f32 GEMMs; "x3" = the split-bf16 GEMM
+    def __init__(self, sd: dict, dtype=torch.float16, device="cuda", gemm="exact", **cfg):
+        """dtype: torch.float16 (the fast path's default since round 6: fp16 activations / weights / MFMA operands,
+        fp32 accumulation and statistics), torch.bfloat16 (the same kernels on bf16) or torch.float32.
+        gemm (fp32 only): "exact" = v_mfma_f32_16x16x4_f32 GEMMs; "x3" = the split-bf16 GEMM
         (ops.split_weight, three bf16 products per K-tile) for every conv: the ResBlock, input and pyramid-head
         convs and (round 5) the attention projections NIN_0..3 and the attention core (split q, k, v, p)."""
         if not torch.cuda.is_available():
@@ -211,7 +213,7 @@ class NCSNppHIP:
 
     def _resblock(self, m, x0, x1, dense, comb=None, comb_w=None, comb_b=None):
         """x0/x1: (tensor, stats) of the (possibly concatenated) input.
-        Where the halo GEMM applies (bf16, 3x3, H%4 == 0, W%64 == 0) GroupNorm+SiLU is fused
+        Where the halo GEMM applies (16-bit, 3x3, H%4 == 0, W%64 == 0) GroupNorm+SiLU is fused
         into the GEMM's halo load; otherwise it is one gn_apply pass (with the FIR for up/down)."""
         e = self.mw[m.idx]
         mode = "up" if m.up else ("down" if m.down else "none")
@@ -285,7 +287,7 @@ class NCSNppHIP:
     def _pyramid(self, x, y, t):
         W = self.W
         dense = self.temb(t)
-        if self.dtype == torch.bfloat16 and ops.input_conv_ok(x) and not _NO_FUSED_INPUT:
+        if self.dtype in ops.H16 and ops.input_conv_ok(x) and not _NO_FUSED_INPUT:
             ht, hst, pyr_in = ops.input_conv(x, y, W["in_w"], W["in_b"])
             h = (ht, hst)
         elif self.gemm == "x3" and ops.input_conv_x3_ok(x) and not _NO_FUSED_INPUT:

@@ -26,8 +26,10 @@ import torch
 
 from . import _lib
 
-F32, BF16 = _lib.F32, _lib.BF16
+F32, BF16, F16 = _lib.F32, _lib.BF16, _lib.F16
 INV_SQRT2 = 1.0 / math.sqrt(2.0)
+# the 16-bit activation / weight formats of the fast path: fp16 (round 6 default) and bf16 (the same kernels)
+H16 = (torch.float16, torch.bfloat16)
 
 
 def conv_code(act_dtype: torch.dtype, wgt_dtype: torch.dtype) -> int:
@@ -55,6 +57,8 @@ def split_weight(w: torch.Tensor) -> torch.Tensor:
 def code(dtype: torch.dtype) -> int:
     if dtype == torch.float32:
         return F32
+    if dtype == torch.float16:
+        return F16
     if dtype == torch.bfloat16:
         return BF16
     raise TypeError(f"snrse: unsupported dtype {dtype}")
@@ -252,7 +256,7 @@ def halo_ok(x, ksize, cout):
     B, H, W, C = x.shape
     # images tileable by 4 x 64 (the kernel then uses 8 x 32 tiles where H % 8 == 0); W = 32 alone stays on
     # the split-K GEMM (faster there: profiles/r03v_level4_halo_vs_glds.jsonl)
-    return (x.dtype == torch.bfloat16 and ksize == 3 and cout % 128 == 0 and H % 4 == 0 and W % 64 == 0
+    return (x.dtype in H16 and ksize == 3 and cout % 128 == 0 and H % 4 == 0 and W % 64 == 0
             and _opt(x, "conv_variant") in (0, 5))
 
 
@@ -270,15 +274,17 @@ def x3h_ok(x, ksize, cout):
 
 def head_ok(x, split=False):
     """True when a 3x3 conv of x with Cout = 4 and f32 output (the pyramid heads) takes a head kernel that
-    accepts a fused GroupNorm (gn=): the halo-staged head (bf16 x, or f32 x with split weights: split=True, the
-    fp32x3 mode's conv_head_x3_kernel; H % 8 == 0, W % 32 == 0), or with C % 256 == 0 the wave-per-8-pixels
-    head of the other image sizes (bf16, or the fp32x3 form; option head_small, snrse_conv2d)."""
+    accepts a fused GroupNorm (gn=): the halo-staged head (16-bit x, C <= 1024; or f32 x with split weights:
+    split=True, the fp32x3 mode's conv_head_x3_kernel; H % 8 == 0, W % 32 == 0), or with C % 256 == 0 the
+    wave-per-8-pixels head of the other image sizes (16-bit, or the fp32x3 form; option head_small, snrse_conv2d)."""
     B, H, W, C = x.shape
     if _opt(x, "conv_variant") == 1:
         return False
-    dt_ok = x.dtype == torch.bfloat16 or (split and x.dtype == torch.float32)
-    # channels: the C-ABI's K-tile (64 bf16 / 32 f32 channels, snrse_conv2d)
-    if dt_ok and H % 8 == 0 and W % 32 == 0 and C % (64 if x.dtype == torch.bfloat16 else 32) == 0:
+    h16 = x.dtype in H16
+    dt_ok = h16 or (split and x.dtype == torch.float32)
+    # channels: the C-ABI's K-tile (64 16-bit / 32 f32 channels, snrse_conv2d); the 16-bit tiled heads stage the
+    # image's GroupNorm affine in an LDS table of 1024 channels
+    if dt_ok and H % 8 == 0 and W % 32 == 0 and C % (64 if h16 else 32) == 0 and (not h16 or C <= 1024):
         return True
     return dt_ok and C % 256 == 0 and _opt(x, "head_small") != 0
 
@@ -426,9 +432,9 @@ def gn_apply(src0, src1=None, sums=None, gamma=None, beta=None, act=True, mode="
 
 
 def resample_ok(x):
-    """True when snrse_gn_resample takes x (NHWC): bf16 with C % 16 == 0, or f32 with C / 4 dividing 64."""
+    """True when snrse_gn_resample takes x (NHWC): 16-bit with C % 16 == 0, or f32 with C / 4 dividing 64."""
     C = x.shape[3]
-    if x.dtype == torch.bfloat16:
+    if x.dtype in H16:
         return C % 16 == 0
     return x.dtype == torch.float32 and C % 4 == 0 and 64 % (C // 4) == 0
 
@@ -436,11 +442,11 @@ def resample_ok(x):
 def gn_resample(x, scale=None, shift=None, act=True, mode="down", want_raw=False):
     """act(x*scale+shift) FIR-resampled x2 ('down' / 'up': upfirdn2d with [1,3,3,1]) and, with
     want_raw, the FIR of x itself (the ResBlock shortcut input) from one LDS-tiled pass over x
-    (snrse_gn_resample; bf16: C % 8 == 0 with C / 8 dividing 64, or C % 16 == 0; f32: C / 4 dividing 64).
+    (snrse_gn_resample; 16-bit: C % 8 == 0 with C / 8 dividing 64, or C % 16 == 0; f32: C / 4 dividing 64).
     Returns (activated, raw or None)."""
     _dev(x, scale, shift)
-    if x.dtype not in (torch.bfloat16, torch.float32):
-        raise TypeError("snrse: gn_resample takes bf16 or f32 activations")
+    if x.dtype not in (torch.float16, torch.bfloat16, torch.float32):
+        raise TypeError("snrse: gn_resample takes fp16, bf16 or f32 activations")
     B, H, W, C = x.shape
     m = MODES[mode]
     if m == 0:
@@ -454,7 +460,7 @@ def gn_resample(x, scale=None, shift=None, act=True, mode="down", want_raw=False
 
 
 def gn_act(src0, src1=None, scale=None, shift=None, act=True):
-    """act(x*scale+shift) of the channel concatenation (src0 | src1), NHWC bf16 or f32 (snrse_gn_act)."""
+    """act(x*scale+shift) of the channel concatenation (src0 | src1), NHWC fp16, bf16 or f32 (snrse_gn_act)."""
     _dev(src0, src1, scale, shift)
     B, H, W, C0 = src0.shape
     C1 = 0 if src1 is None else src1.shape[3]
@@ -516,16 +522,19 @@ def input_conv_ok(x):
 
 
 def input_conv(x, y, wgt, bias):
-    """bf16 fused input conv: x, y complex64 [B,F,T] -> (h [B,F,T,128] bf16, stats, pyramid f32)."""
+    """16-bit fused input conv: x, y complex64 [B,F,T], wgt [128][64] fp16 or bf16 -> (h [B,F,T,128] in wgt's
+    format, stats, pyramid f32)."""
     _dev(x, y, wgt, bias)
+    if wgt.dtype not in H16:
+        raise TypeError(f"snrse: input_conv takes fp16 / bf16 weights, got {wgt.dtype}")
     B, F, T = x.shape[0], x.shape[-2], x.shape[-1]
-    h = torch.empty(B, F, T, 128, device=x.device, dtype=torch.bfloat16)
+    h = torch.empty(B, F, T, 128, device=x.device, dtype=wgt.dtype)
     pyr = torch.empty(B, F, T, 4, device=x.device, dtype=torch.float32)
     st = new_stats(B, 128)
     cx = context(x.device)
     _stats_zeroed(cx, st)
     _lib.call("snrse_input_conv", cx.ptr, x.data_ptr(), y.data_ptr(), B, F, T, wgt.data_ptr(), bias.data_ptr(),
-              h.data_ptr(), pyr.data_ptr(), st.data_ptr(), _stream())
+              h.data_ptr(), pyr.data_ptr(), st.data_ptr(), code(wgt.dtype), _stream())
     return h, st, pyr
 
 

@@ -43,11 +43,12 @@ def _run_threads(fns):
     return outs
 
 
-@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+@pytest.mark.parametrize("dt", ["fp32", "fp16", "bf16"])
 def test_two_threads_network_evaluations_match_serial(gpu, dt):
     from snrse import ncsnpp
     sd = {k: torch.from_numpy(v) for k, v in formula_sd("ncsnpp").items()}
-    net = ncsnpp.NCSNppHIP(sd, dtype=torch.float32 if dt == "fp32" else torch.bfloat16, device=gpu)
+    net = ncsnpp.NCSNppHIP(sd, dtype={"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}[dt],
+                           device=gpu)
     ins = []
     for k in range(2):
         x = torch.from_numpy(fnormal(f"reentrant.x{k}", (2, 2, 256, 64), complex_=True)) * 0.5

@@ -60,4 +60,5 @@ def test_resample_shape_contract():
     assert ok(128, torch.bfloat16) and ok(256, torch.bfloat16) and not ok(8, torch.bfloat16)
     assert ok(4, torch.float32) and ok(128, torch.float32) and ok(256, torch.float32)
     assert not ok(512, torch.float32) and not ok(12, torch.float32) and not ok(6, torch.float32)
-    assert not ok(128, torch.float16)
+    assert ok(128, torch.float16) and not ok(8, torch.float16)  # fp16: the 16-bit path's format since round 6
+    assert not ok(128, torch.float64)
