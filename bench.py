@@ -498,14 +498,23 @@ def run_train(args):
 
 
 # ----------------------------------------------------------------------------- GPU bench
+# rocprofv3 --kernel-trace --marker-trace --selected-regions collects only between roctxProfilerResume(0) and
+# roctxProfilerPause(0); the roctx library is loaded before anything touches the GPU (loaded later, or without
+# --marker-trace, the region collected nothing: profiles/r06d_roctx_region_check.txt)
+_ROCTX = None
+if os.environ.get("SNRSE_ROCTX") == "1":
+    import ctypes as _ct
+    _ROCTX = _ct.CDLL("librocprofiler-sdk-roctx.so")
+    _ROCTX.roctxProfilerResume.argtypes = [_ct.c_uint64]
+    _ROCTX.roctxProfilerPause.argtypes = [_ct.c_uint64]
+
+
 def roctx_region():
     """f(True) / f(False): roctxProfilerResume(0) / roctxProfilerPause(0) around the timed steps when SNRSE_ROCTX=1, so
-    `rocprofv3 --selected-regions` collects exactly the timed kernels; a no-op otherwise."""
-    if os.environ.get("SNRSE_ROCTX") != "1":
+    the rocprof summary holds exactly the timed kernels; a no-op otherwise."""
+    if _ROCTX is None:
         return lambda on: None
-    import ctypes
-    lib = ctypes.CDLL("librocprofiler-sdk-roctx.so")
-    return lambda on: (lib.roctxProfilerResume if on else lib.roctxProfilerPause)(ctypes.c_uint64(0))
+    return lambda on: (_ROCTX.roctxProfilerResume if on else _ROCTX.roctxProfilerPause)(0)
 
 
 # c2 / c4: the configuration's 16-bit arithmetic, in IEEE fp16 since round 6 (same bytes and MFMA rate as bf16;
@@ -635,6 +644,29 @@ def run(args):
             and args.seconds == 4.0 and args.N == 30):
         del enh, probe_enh, net
         torch.cuda.empty_cache()
+        fcost = None
+        if args.dtype == "fp16":
+            # what the fp16 headline costs against the bf16 form of the same kernels (round 6): one warm-up + 3 timed
+            # bf16 steps on the same clips and seeds, and bf16's own N=5 PC golden error beside fp16's
+            import paritycheck
+            netb = ncsnpp.NCSNppHIP(formula_weights(), dtype=torch.bfloat16, device=dev)
+            enhb = PCEnhancer(netb, sde, N=args.N)
+            enhb(y, noise(50))
+            torch.cuda.synchronize()
+            tb = time.perf_counter()
+            for k in range(3):
+                enhb(y, noise(100 + k))
+            torch.cuda.synchronize()
+            vb = 3 * B / (time.perf_counter() - tb)
+            fcost = {"what": "the same C2 step with bf16 activations / weights / MFMA operands (same kernels)",
+                     "bf16_value": vb, "bf16_steps": 3, "fp16_over_bf16": value / vb}
+            if not args.no_parity:
+                rb = paritycheck.pc_vs_golden(dev, netb)
+                fcost["bf16_pc_rel_rms"] = rb["rel_rms"]
+                fcost["fp16_pc_rel_rms"] = parity["rel_rms"] if parity else None
+                fcost["tol_rel"] = paritycheck.TOL["pc"]["fp16"]
+            del enhb, netb
+            torch.cuda.empty_cache()
         net3 = ncsnpp.NCSNppHIP(formula_weights(), dtype=torch.float32, device=dev, gemm="x3")
         enh3 = PCEnhancer(net3, sde, N=args.N)
         K3 = max(3, args.steps)
@@ -646,7 +678,7 @@ def run(args):
         torch.cuda.synchronize()
         el3 = time.perf_counter() - t3
         pmode = {"dtype": "fp32x3", "value": K3 * B / el3, "unit": "utt/s", "ms_per_step": el3 / K3 * 1e3,
-                 "steps": K3, "warmup": 1,
+                 "steps": K3, "warmup": 1, "format_cost": fcost,
                  "note": ("fp32 activations / storage / accumulation, ResBlock and input convs as "
                           "split-bf16 GEMMs (bench.py --dtype fp32x3 for the full line)")}
         # the x3 output for the 16-bit timed run's last seed (100 + steps - 1): the K3-th timed step when
