@@ -1599,7 +1599,10 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
 #ifdef SNRSE_STAMPS
-  unsigned long long* const lst = (unsigned long long*)(ring + 2 * SLOT) + wid * 32;
+  // past both the main-loop layout and the epilogue's staging + statistics area (which reuses the ring)
+  constexpr int kStampOff = (HALO_BYTES + 2 * SLOT + 1280) > (4 * (64 * 68 * 4) + 4 * 128 * 2 * 4)
+                                ? (HALO_BYTES + 2 * SLOT + 1280) : (4 * (64 * 68 * 4) + 4 * 128 * 2 * 4);
+  unsigned long long* const lst = (unsigned long long*)(smem + kStampOff) + wid * 32;
 #endif
   SNRSE_STAMP(0);
   const int nb = gridDim.x, bid = blockIdx.x;
@@ -1953,7 +1956,11 @@ int launch_halo5_ef(ConvParams p, int grid, hipStream_t s) {
   // and at least the epilogue's reuse of it: 4 waves' 64 x 68 f32 staging + the 4 x 128 x 2 f32 statistics
   constexpr size_t main_lds = (256 / TW + 2) * (TW + 2) * 64 + 2 * 3 * 128 * 64 + 1024 + 256;
   constexpr size_t epi_lds = 4 * (64 * 68 * 4) + 4 * 128 * 2 * 4;
+#ifdef SNRSE_STAMPS
+  constexpr size_t lds = (main_lds > epi_lds ? main_lds : epi_lds) + 1024;  // + the 4 waves' stamps (kStampOff)
+#else
   constexpr size_t lds = main_lds > epi_lds ? main_lds : epi_lds;
+#endif
   static const hipError_t attr = hipFuncSetAttribute((const void*)conv_halo5_kernel<T, TO, GNM, EF, TW, SCD>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   SNRSE_RET(attr);  // (thread-safe one-time set: a function-local static)
