@@ -51,8 +51,6 @@ int* option_field(snrse_ctx& c, const char* name) {
   if (name_is(name, "epi_nt_mb")) return &c.epi_nt_mb;
   if (name_is(name, "h5_specialise")) return &c.h5_specialise;
   if (name_is(name, "h5_tw")) return &c.h5_tw;
-  if (name_is(name, "h5_persist")) return &c.h5_persist;
-  if (name_is(name, "h5_stagger")) return &c.h5_stagger;
   if (name_is(name, "stats_zeroed")) return &c.stats_zeroed;
   if (name_is(name, "resample_variant")) return &c.resample_variant;
   if (name_is(name, "resample_nt")) return &c.resample_nt;

@@ -183,9 +183,6 @@ struct snrse_ctx {
   int h5_specialise = 1;       // compile-time epilogue flags for the common bf16 (halo GEMM) and fp32x3 (x3h pair
                                // schedule) ResBlock configurations
   int h5_tw = 0;               // halo tile width: 0 auto (32 where H % 8 == 0), 64, 32
-  int h5_stagger = 0;          // persistent halo GEMM: start delay of the grid's second half (x 127 x 64 cycles)
-  int h5_persist = 0;          // halo GEMM without a fused shortcut, 16-bit output: 1 the persistent form
-                               // (conv_halo5p_kernel, round 6: the next tile's first halo and weights under the epilogue)
   int stats_zeroed = 0;        // statistics buffers arrive zeroed (the caller clears one arena)
   int resample_variant = 0;    // 0 row-strip, 1 LDS-tiled gn_resample
   int resample_nt = 0;         // non-temporal stores in gn_resample

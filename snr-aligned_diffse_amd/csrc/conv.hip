@@ -1968,368 +1968,6 @@ int launch_halo5_ef(ConvParams p, int grid, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------------------------
-// Round 6: the persistent form of the halo GEMM for the convs without a fused shortcut (the Conv_0s and the residual
-// Conv_1s).  The launch is 2 workgroups per CU; each walks tiles g, g + G, g + 2G, ... (G = the grid, g the XCD-aware
-// logical id, so the 64 workgroups of an XCD work on 64 neighbouring tiles at each step).  Per tile the chunk / phase loop
-// is conv_halo5_kernel's; what changes is the tile boundary.  In the one-tile-per-workgroup kernel every tile starts
-// with an exposed prologue -- the first chunk's halo from HBM, its GroupNorm affine, the first weight phase -- measured
-// at 11.5 % of a workgroup's life at level 0 (+ 2.5 % first-phase wait; profiles/r06f_halo5_stamps.jsonl), during which
-// the CU's other workgroup runs alone.  Here the next tile's first weight phase is requested into ring slot 1 and its
-// first halo into registers before / during the current tile's epilogue, which stages its accumulators 32 rows at a time
-// (35 KB instead of 70 KB, epilogue_img_rs) so that slot 1 is not overwritten; the tile's phases then run with the
-// ring parity flipped (slot of phase q = (q + par) & 1).  After the epilogue only the GroupNorm transform + LDS store of
-// the first chunk remain before the next tile's MFMAs.
-template <typename TO, int EF, int TW, typename F>
-SNRSE_DEV void epilogue_img_rs(const ConvParams& p, const f32x4 (&acc)[4][4], int mb, int nb, int lane, float* stage,
-                               float* red, int wm, int blk_n0, int seg_skip, const float* pre_add, F&& after_issue) {
-  const bool f_res = EF < 0 ? p.res != nullptr : (EF & EF_RES) != 0;
-  const bool f_comb = EF < 0 ? p.comb_src != nullptr : (EF & EF_COMB) != 0;
-  const bool f_stats = EF < 0 ? p.stats != nullptr : (EF & EF_STATS) != 0;
-  const bool f_nt = EF < 0 ? p.epi_nt != 0 : (EF & EF_NT) != 0;
-  static_assert(sizeof(TO) == 2, "16-bit output");
-  constexpr int LDR = 68;
-  constexpr int EPC = 8, NCH = 8, RPP = 8, NPASS = 8;  // a lane: 8 channels (one 16-B chunk) of rows r0 + 8 pass
-  const int lrow = lane & 15, lg = lane >> 4;
-  const int cc = lane % NCH, r0 = lane / NCH;
-  const int n = nb + cc * EPC;
-  float add[EPC];
-#pragma unroll
-  for (int k = 0; k < EPC; ++k) add[k] = pre_add[k];
-  float cw[EPC][4], cb[EPC];
-  if (f_comb) {
-#pragma unroll
-    for (int k = 0; k < EPC; ++k) {
-      const f32x4 w = *(const f32x4*)(p.comb_w + (size_t)(n + k) * 4);
-      cw[k][0] = w[0]; cw[k][1] = w[1]; cw[k][2] = w[2]; cw[k][3] = w[3];
-      cb[k] = p.comb_b[n + k];
-    }
-  }
-  float s1[EPC], s2[EPC];
-#pragma unroll
-  for (int k = 0; k < EPC; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
-  u32x4 rpre[NPASS];
-  f32x4 qpre[NPASS];
-#pragma unroll
-  for (int pass = 0; pass < NPASS; ++pass) {
-    const size_t m = (size_t)epi_pix<TW>(mb, r0 + pass * RPP, seg_skip);
-    if (f_res) rpre[pass] = *(const u32x4*)((const TO*)p.res + m * p.res_ld + n);
-    if (f_comb) qpre[pass] = *(const f32x4*)(p.comb_src + m * 4);
-  }
-  after_issue();
-#pragma unroll
-  for (int rh = 0; rh < 2; ++rh) {
-    if (rh == 1) {  // every lane's reads of the first row half are done before it is overwritten
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_wave_barrier();
-    }
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) stage[(ii * 16 + lg * 4 + e) * LDR + j * 16 + lrow] = acc[2 * rh + ii][j][e];
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int ps = 0; ps < NPASS / 2; ++ps) {
-      const int pass = rh * (NPASS / 2) + ps;
-      const int row = r0 + pass * RPP;
-      const size_t m = (size_t)epi_pix<TW>(mb, row, seg_skip);
-      float v[EPC];
-      const float* sr = stage + (r0 + ps * RPP) * LDR + cc * EPC;
-#pragma unroll
-      for (int k = 0; k < EPC; ++k) v[k] = sr[k] + add[k];
-      if (f_res) {
-        const u32x4 rv = rpre[pass];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          v[2 * k] += H16<TO>::lo(rv[k]);
-          v[2 * k + 1] += H16<TO>::hi(rv[k]);
-        }
-      }
-      if (p.out_scale != 1.f) {
-#pragma unroll
-        for (int k = 0; k < EPC; ++k) v[k] *= p.out_scale;
-      }
-      if (f_comb) {
-        const f32x4 q = qpre[pass];
-#pragma unroll
-        for (int k = 0; k < EPC; ++k) v[k] += q[0] * cw[k][0] + q[1] * cw[k][1] + q[2] * cw[k][2] + q[3] * cw[k][3] + cb[k];
-      }
-      const u32x4 o = pack8<TO>(v);
-      if (f_nt)
-        __builtin_nontemporal_store(o, (u32x4*)((TO*)p.out + m * p.out_ld + n));
-      else
-        *(u32x4*)((TO*)p.out + m * p.out_ld + n) = o;
-      if (f_stats) {
-#pragma unroll
-        for (int k = 0; k < EPC; ++k) { s1[k] += v[k]; s2[k] = fmaf(v[k], v[k], s2[k]); }
-      }
-    }
-  }
-  if (f_stats) {
-#pragma unroll
-    for (int k = 0; k < EPC; ++k) {
-      s1[k] = sum_lanes_strided<NCH>(s1[k]);
-      s2[k] = sum_lanes_strided<NCH>(s2[k]);
-    }
-    if (r0 == 0) {
-#pragma unroll
-      for (int k = 0; k < EPC; ++k) {
-        red[(wm * 128 + nb - blk_n0 + cc * EPC + k) * 2] = s1[k];
-        red[(wm * 128 + nb - blk_n0 + cc * EPC + k) * 2 + 1] = s2[k];
-      }
-    }
-  }
-}
-
-template <typename T, typename TO, int GNM, int EF, int TW>
-__global__ __launch_bounds__(256, 2) void conv_halo5p_kernel(ConvParams p, int ntiles) {
-  constexpr int TH = 256 / TW, HC = TW + 2;
-  constexpr int RW = TH / 4;
-  constexpr int HROWS = (TH + 2) * HC;
-  constexpr int HJ = (HROWS + 63) / 64;
-  constexpr int HALO_BYTES = HROWS * 64;
-  constexpr int TAPB = 128 * 64;
-  constexpr int SLOT = 3 * TAPB;
-  constexpr int KT = 32;
-  constexpr int STG = 32 * 68 * 4;  // a wave's row-half staging area (epilogue_img_rs)
-  static_assert(4 * STG + 4 * 128 * 2 * 4 <= HALO_BYTES + SLOT, "the epilogue must leave ring slot 1 alone");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const halo = smem;
-  char* const ring = smem + HALO_BYTES;
-  float* const gnl = (float*)(smem + HALO_BYTES + 2 * SLOT + 1024);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int G = gridDim.x, bid = blockIdx.x;
-  const int q8 = G >> 3, r8 = G & 7, xcd = bid & 7, pos = bid >> 3;
-  int t = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + pos;
-  if (t >= ntiles) return;  // (the launcher keeps G <= ntiles)
-  const int ntw = p.W / TW, nth = p.H / TH;
-  const int Cin = p.C0 + p.C1;
-  const int cbm = Cin / KT;
-  const int nq = 3 * cbm;
-  const int K1 = 9 * Cin;
-  const int hcol = tid & 3;
-  int n0, w0, h0, bb;
-  auto coords = [&](int tt) {
-    n0 = (tt % p.ntn) * 128;
-    tt /= p.ntn;
-    w0 = (tt % ntw) * TW;
-    tt /= ntw;
-    h0 = (tt % nth) * TH;
-    bb = tt / nth;
-  };
-  int hpix[HJ];
-  bool hok[HJ];
-  auto set_pix = [&]() {
-#pragma unroll
-    for (int j = 0; j < HJ; ++j) {
-      const int hr = (tid >> 2) + 64 * j;
-      const int hy = hr / HC, hx = hr - (hr / HC) * HC;
-      const int ih = h0 + hy - 1, iw = w0 + hx - 1;
-      hok[j] = hr < HROWS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
-      hpix[j] = (bb * p.H + ih) * p.W + iw;
-    }
-  };
-  u32x4 hv[HJ];
-  f32x4 gnv;
-  auto halo_load = [&](int c) {
-    const int ch = c * KT;
-    const bool s1 = ch >= p.C0;
-    const __amdgpu_buffer_rsrc_t r_ = make_rsrc(s1 ? p.src1 : p.src0, s1 ? p.bytes1 : p.bytes0);
-    const int cs_ = s1 ? p.C1 : p.C0, cc_ = (s1 ? ch - p.C0 : ch) + hcol * 8;
-#pragma unroll
-    for (int j = 0; j < HJ; ++j) {
-      const int voff_ = hok[j] ? (hpix[j] * cs_ + cc_) * 2 : (int)0x80000000;
-      hv[j] = __builtin_amdgcn_raw_buffer_load_b128(r_, voff_, 0, 0);
-    }
-    if constexpr (GNM > 0) {
-      if (tid < 16) gnv = *(const f32x4*)((tid < 8 ? p.gn_scale : p.gn_shift) + (size_t)bb * Cin + ch + (tid & 7) * 4);
-    }
-  };
-  auto gn_publish = [&]() {
-    if constexpr (GNM > 0) {
-      if (tid < 16) {
-        f32x4 g = gnv;
-        if constexpr (GNM == 2) g *= kNegLog2e;
-        *(f32x4*)(gnl + tid * 4) = g;
-      }
-    }
-  };
-  auto halo_store = [&]() {
-    float gsc[8], gsh[8];
-    if constexpr (GNM > 0) {
-      const f32x4 s0 = *(const f32x4*)(gnl + hcol * 8), s1 = *(const f32x4*)(gnl + hcol * 8 + 4);
-      const f32x4 t0 = *(const f32x4*)(gnl + 32 + hcol * 8), t1 = *(const f32x4*)(gnl + 32 + hcol * 8 + 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { gsc[i] = s0[i]; gsc[4 + i] = s1[i]; gsh[i] = t0[i]; gsh[4 + i] = t1[i]; }
-    }
-#pragma unroll
-    for (int j = 0; j < HJ; ++j) {
-      const int hr = (tid >> 2) + 64 * j;
-      if (j == HJ - 1 && hr >= HROWS) break;
-      u32x4 v = hv[j];
-      if constexpr (GNM > 0) v = gn_xform8<T, GNM>(v, gsc, gsh, hok[j]);
-      *(u32x4*)(halo + swz64(hr, hcol)) = v;
-    }
-  };
-  // 3 weight taps of phase group g of chunk c for output channels n0.. into ring slot dst (oob: the same 6 pieces per
-  // wave out of range, a fixed count for the compiler's waitcnt model)
-  auto dma = [&](int c, int g, char* dst, bool oob) {
-    const int rl = lane >> 2, sl = lane & 3;
-    const unsigned oobm = oob ? 0x80000000u : 0u;
-    const __amdgpu_buffer_rsrc_t r = make_rsrc(p.wgt, p.wbytes);
-    const int kb = c * KT;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const int ii = wid + 4 * k;
-      const int jt = ii >> 3, pc = ii & 7;
-      const int row = pc * 16 + rl;
-      const unsigned voff = oobm | (unsigned)(((n0 + row) * K1 + (3 * g + jt) * Cin + kb + (sl ^ ((row >> 1) & 3)) * 8) * 2);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(dst + jt * TAPB + pc * 1024),
-                                               16, voff, 0, 0, 0);
-    }
-  };
-  auto vm_after_dma = [&]() { __builtin_amdgcn_s_waitcnt(0x0f76); };
-  const int lrow = lane & 15, lg = lane >> 4;
-  const bool w0g = GNM > 0 && wid == 0;
-
-  // the CU's two workgroups would otherwise run their tiles in lock step (same work per tile), prologue on prologue and
-  // epilogue on epilogue; the second half of the grid starts later by p.stagger x 127 x 64 cycles
-  if (bid >= G / 2 && p.stagger > 0) {
-    for (int k = 0; k < p.stagger; ++k) __builtin_amdgcn_s_sleep(127);
-  }
-  coords(t);
-  set_pix();
-  halo_load(0);
-  dma(0, 0, ring, false);
-  if constexpr (GNM > 0) {
-    gn_publish();
-    __syncthreads();
-  }
-  halo_store();
-  int par = 0;
-  for (;;) {
-    f32x4 acc[2][4][4];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bool halo_inflight = false;
-    for (int q = 0; q < nq; ++q) {
-      const int c = q / 3, t0 = (q - c * 3) * 3;
-      const bool first = t0 == 0, last = t0 == 6;
-      if (q == 0 && par) {
-        // the first phase's weights were requested before the previous tile's epilogue; newer than them are that
-        // epilogue's 16 output stores (+ its statistics atomic), which need not land now
-        asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)" ::: "memory");
-      } else if (halo_inflight) {
-        if (w0g) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(HJ + 1) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(HJ) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
-      dma(q + 1 < nq ? (q + 1) / 3 : 0, (q + 1) % 3, ring + ((q + 1 + par) & 1) * SLOT, q + 1 >= nq);
-      halo_inflight = false;
-      if (first && c + 1 < cbm) {
-        vm_after_dma();
-        halo_load(c + 1);
-        halo_inflight = !last && q + 1 < nq;
-      }
-      const char* sl = ring + ((q + par) & 1) * SLOT;
-      for (int jt = 0; jt < 3; ++jt) {
-        const int tp = t0 + jt;
-        const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
-        const int hbase = (wid * RW + dy + 1) * HC + dx + 1 + lrow;
-        const char* sb = sl + jt * TAPB;
-        u32x4 af[4], bfr[8];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = *(const u32x4*)(halo + swz64(hbase + (16 * i / TW) * HC + (16 * i) % TW, lg));
-#pragma unroll
-        for (int j = 0; j < 8; ++j) bfr[j] = *(const u32x4*)(sb + swz64(j * 16 + lrow, lg));
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[h][i][j] = mfma_chunk<T>(af[i], bfr[h * 4 + j], acc[h][i][j]);
-      }
-      if (last && c + 1 < cbm) {
-        gn_publish();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        vm_after_dma();
-        halo_store();
-      }
-    }
-    // ---- tile end: this tile's bias + temb, then (after the barrier that frees the halo and both ring slots) the next
-    // tile's first weight phase into slot 1, the epilogue, whose first half requests the next tile's first halo
-    float add0[8], add1[8];
-    epi_add<TO, EF>(p, n0, lane, bb, add0);
-    epi_add<TO, EF>(p, n0 + 64, lane, bb, add1);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const int cn0 = n0, cbb = bb;
-    const int mrow = (bb * p.H + h0 + wid * RW) * p.W + w0;
-    const int tn = t + G;
-    const bool more = tn < ntiles;
-    if (more) {
-      coords(tn);
-      dma(0, 0, ring + SLOT, false);
-    }
-    float* const stage = (float*)(smem + wid * STG);
-    float* const red = (float*)(smem + 4 * STG);
-    epilogue_img_rs<TO, EF, TW>(p, acc[0], mrow, cn0, lane, stage, red, wid, cn0, p.W - TW, add0, []() {});
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    epilogue_img_rs<TO, EF, TW>(p, acc[1], mrow, cn0 + 64, lane, stage, red, wid, cn0, p.W - TW, add1, [&]() {
-      if (more) {
-        set_pix();
-        halo_load(0);
-      }
-    });
-    if (EF < 0 ? p.stats != nullptr : (EF & EF_STATS) != 0) {
-      // (block_stats_flush with the compile-time trip count of 256 threads x 2 x 128 values: one atomic per thread)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      const int slot = blockIdx.x & (SNRSE_STAT_SLOTS - 1);
-      float a = 0.f;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) a += red[w * 256 + tid];
-      unsafeAtomicAdd(&p.stats[stat_idx(cbb, slot, cn0 + (tid >> 1), p.Cout) + (tid & 1)], (double)a);
-    }
-    if (!more) break;
-    t = tn;
-    par = 1;
-    gn_publish();
-    __syncthreads();  // every wave is done with the staging / statistics area (the halo region); the affine is in LDS
-    halo_store();
-  }
-}
-
-template <typename T, typename TO, int GNM, int EF, int TW>
-int launch_halo5p_ef(ConvParams p, int tiles, hipStream_t s) {
-  constexpr size_t lds = (256 / TW + 2) * (TW + 2) * 64 + 2 * 3 * 128 * 64 + 1024 + 256;
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_halo5p_kernel<T, TO, GNM, EF, TW>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  SNRSE_RET(attr);
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    SNRSE_RET(hipGetDevice(&dev));
-    SNRSE_RET(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  const int grid = p.stagger < 0 ? tiles : std::min(tiles, 2 * ncu);  // (stagger < 0: one tile per workgroup, A/B)
-  hipLaunchKernelGGL((conv_halo5p_kernel<T, TO, GNM, EF, TW>), dim3(grid), dim3(256), lds, s, p, tiles);
-  return (int)hipGetLastError();
-}
-
 template <typename T, typename TO, int GNM, int TW>
 int launch_halo5_gn(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   p.ntn = p.Cout / 128;
@@ -2343,23 +1981,6 @@ int launch_halo5_gn(ConvParams p, hipStream_t s, snrse_ctx& cx) {
   const bool scd = p.sc_src != nullptr;  // the fused shortcut's chunks as LDS-DMA phases
   // the 16-bit ResBlock configurations of the NCSN++ path get a branch-free epilogue (bias always on):
   // Conv_0 (+temb), Conv_1 (+residual | +1x1 shortcut as extra K | +Combine), each +-stats, +-NT
-  // the persistent form (option h5_persist, round 6) for the convs without a fused shortcut: fp16, 8 x 32 tiles
-  if constexpr (sizeof(TO) == 2 && std::is_same_v<T, f16_t> && TW == 32) {
-    if (cx.h5_persist && !scd) {
-      cx.last_kernel = 6;
-      p.stagger = cx.h5_stagger;
-      if (GNM != 1 && cx.h5_specialise && p.bias) {
-        switch (epi_flags(p)) {
-          case EF_TEMB | EF_STATS: return launch_halo5p_ef<T, TO, GNM, EF_TEMB | EF_STATS, TW>(p, tiles, s);
-          case EF_TEMB | EF_STATS | EF_NT: return launch_halo5p_ef<T, TO, GNM, EF_TEMB | EF_STATS | EF_NT, TW>(p, tiles, s);
-          case EF_RES | EF_STATS: return launch_halo5p_ef<T, TO, GNM, EF_RES | EF_STATS, TW>(p, tiles, s);
-          case EF_RES | EF_STATS | EF_NT: return launch_halo5p_ef<T, TO, GNM, EF_RES | EF_STATS | EF_NT, TW>(p, tiles, s);
-          default: break;
-        }
-      }
-      return launch_halo5p_ef<T, TO, GNM, EF_RT, TW>(p, tiles, s);
-    }
-  }
   if constexpr (sizeof(TO) == 2 && GNM != 1) {
     if (cx.h5_specialise && p.bias) {
 #define SNRSE_H5_EF(F) \

@@ -50,7 +50,6 @@ struct ConvParams {
   int ksplit;             // K splits of the v2 GEMM (1: the epilogue runs in the GEMM itself)
   unsigned long long* stamps;  // timing-diagnostic build only (-DSNRSE_STAMPS): [blocks][8][32]
   int epi_nt;      // image-tile epilogue: non-temporal output stores
-  int stagger;     // persistent halo GEMM: start delay of the grid's second half, in units of s_sleep 127 (option h5_stagger)
 };
 
 #ifdef SNRSE_STAMPS

@@ -235,7 +235,7 @@ def probe_read(max_calls, dev=None, all_threads=False):
 
 
 KERNELS = {1: "conv_mfma_kernel", 2: "conv_glds_kernel", 3: "conv_x3_kernel", 4: "conv_x3h_kernel",
-           5: "conv_halo5_kernel", 6: "conv_halo5p_kernel",
+           5: "conv_halo5_kernel",
            10: "conv_head_kernel", 11: "conv_head_x3_kernel", 14: "conv_head_small_kernel",
            15: "conv_head_part_kernel"}
 
