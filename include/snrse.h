@@ -198,7 +198,8 @@ int snrse_temb_mlp(const float* t, const float* Wg, const float* W1, const float
                    const float* b2, float* temb, int B, int nf, hipStream_t stream);
 /* The same MLP as two row-parallel launches (the form the network executor runs; every weight row is read once
  * per launch, spread over the chip): snrse_temb_gfp_dense gives the pre-activation a[b] = W1 [sin, cos](2 pi log t
- * W_gfp) + b1 (out [B][4 nf]), then snrse_temb_dense(a, W2, b2) = W2 silu(a) + b2 = temb.  nf even, 2 nf <= 512. */
+ * W_gfp) + b1 (out [B][4 nf]), then snrse_temb_dense(a, W2, b2) = W2 silu(a) + b2 = temb.  nf even, 4 nf <= 512
+ * (nf <= 128: snrse_temb_dense takes D = 4 nf <= 512; NCSN++ uses nf = 128). */
 int snrse_temb_gfp_dense(const float* t, const float* Wg, const float* W1, const float* b1, float* out, int B, int nf,
                          hipStream_t stream);
 /* All ResBlock Dense_0 projections (layerspp.py:264-265): out[b][r] = W[r] . silu(temb[b]) + bias[r]. */

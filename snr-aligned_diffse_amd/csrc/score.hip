@@ -794,7 +794,8 @@ extern "C" int snrse_temb_mlp(const float* t, const float* Wg, const float* W1, 
 
 extern "C" int snrse_temb_gfp_dense(const float* t, const float* Wg, const float* W1, const float* b1, float* out,
                                     int B, int nf, hipStream_t s) {
-  if (nf <= 0 || 2 * nf > 512 || nf % 2 || B <= 0 || !t || !Wg || !W1 || !b1 || !out) return SNRSE_EINVAL;
+  // 4 nf <= 512: the pair's second launch (snrse_temb_dense, D = 4 nf) holds its input rows in a 512-float table
+  if (nf <= 0 || 4 * nf > 512 || nf % 2 || B <= 0 || !t || !Wg || !W1 || !b1 || !out) return SNRSE_EINVAL;
   return launch_dense<2, 0>(nullptr, t, Wg, W1, b1, out, B, 4 * nf, 2 * nf, s);
 }
 
