@@ -13,6 +13,8 @@ import torch  # noqa: E402
 
 from snrse import ops  # noqa: E402
 
+DT = torch.float16  # the 16-bit format (--dtype)
+
 # (B, C0, C1, Cout, H, W, ksize, Csc) — the dominant per-NFE shapes at 4 s
 SHAPES = [
     (32, 128, 0, 128, 256, 512, 3, 0),
@@ -41,11 +43,11 @@ def _gn_pair(B, C, dev, g):
 def run(shape, variant, reps, dev, gn=False, opt=None):
     B, C0, C1, Co, H, W, k, Csc = shape
     g = torch.Generator(device=dev).manual_seed(0)
-    x0 = torch.randn(B, H, W, C0, device=dev, generator=g).bfloat16()
-    x1 = torch.randn(B, H, W, C1, device=dev, generator=g).bfloat16() if C1 else None
-    sc = torch.randn(B, H, W, Csc, device=dev, generator=g).bfloat16() if Csc else None
-    w = (torch.randn(Co, k * k * (C0 + C1), device=dev, generator=g) / 30).bfloat16()
-    ws = (torch.randn(Co, Csc, device=dev, generator=g) / 16).bfloat16() if Csc else None
+    x0 = torch.randn(B, H, W, C0, device=dev, generator=g).to(DT)
+    x1 = torch.randn(B, H, W, C1, device=dev, generator=g).to(DT) if C1 else None
+    sc = torch.randn(B, H, W, Csc, device=dev, generator=g).to(DT) if Csc else None
+    w = (torch.randn(Co, k * k * (C0 + C1), device=dev, generator=g) / 30).to(DT)
+    ws = (torch.randn(Co, Csc, device=dev, generator=g) / 16).to(DT) if Csc else None
     bias = torch.zeros(Co, device=dev)
     st = ops.new_stats(B, Co)
     gnp = None
@@ -78,7 +80,10 @@ def main():
     ap.add_argument("--shapes", default="", help="comma list of SHAPES indices (default all)")
     ap.add_argument("--gn", action="store_true", help="fused GroupNorm+SiLU prologue (halo kernels)")
     ap.add_argument("--option", default="", help="A/B an option instead of conv_variant: --variants are its values")
+    ap.add_argument("--dtype", default="fp16", choices=("fp16", "bf16"))
     a = ap.parse_args()
+    global DT
+    DT = torch.float16 if a.dtype == "fp16" else torch.bfloat16
     dev = torch.device("cuda")
     res = []
     sel = [SHAPES[int(i)] for i in a.shapes.split(",")] if a.shapes else SHAPES
