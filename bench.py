@@ -413,10 +413,11 @@ class ConvProbe:
         return by
 
 
-def pmc_traffic(kernel_prefix, tag):
+def pmc_traffic(kernel_prefix, tag, dtype=None):
     """HBM bytes per launch of the dominant kernel from the committed PMC profile
     (profiles/*_pmc_traffic.json, tools/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950 correction +
-    WRITE_SIZE) for this config tag; None when absent."""
+    WRITE_SIZE) for this config tag and 16-bit format (profiles before round 6 carry no dtype: bf16);
+    None when absent."""
     def newest_first(path):  # profiles/rNN<suffix>_...: round, then suffix length, then suffix (v < ak)
         tag = os.path.basename(path).split("_")[0]
         m = re.match(r"r(\d+)([a-z]*)$", tag)
@@ -425,7 +426,8 @@ def pmc_traffic(kernel_prefix, tag):
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=newest_first, reverse=True):
         with open(path) as f:
             d = json.load(f)
-        if d.get("kernel", "").startswith(kernel_prefix) and d.get("config", "c2") == tag:
+        if (d.get("kernel", "").startswith(kernel_prefix) and d.get("config", "c2") == tag
+                and (dtype is None or d.get("dtype", "bf16") == dtype)):
             return d.get("bytes_per_launch"), os.path.relpath(path, ROOT)
     return None, None
 
@@ -601,9 +603,10 @@ def run(args):
         fl, ms, n = by[kname]
         ach = fl / (ms * 1e-3) if ms > 0 else 0.0
         peak = PEAK[args.dtype]
-        traffic, tsrc = pmc_traffic(kname, args.config)
+        tdt = args.dtype if args.dtype in ("fp16", "bf16") else None
+        traffic, tsrc = pmc_traffic(kname, args.config, tdt)
         if traffic is None and "+" in kname:  # no family profile: its first kernel's launches
-            traffic, tsrc = pmc_traffic(kname.split("+")[0], args.config)
+            traffic, tsrc = pmc_traffic(kname.split("+")[0], args.config, tdt)
         roof = {"bound": "mfma", "achieved": ach / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
                 "frac": ach / peak, "traffic": traffic, "kernel": kname, "launches_per_pass": n,
                 "avg_launch_us": ms * 1e3 / max(n, 1), "flop_per_launch": fl / max(n, 1),
