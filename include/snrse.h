@@ -175,7 +175,10 @@ int snrse_set_workspace(void* ptr, size_t bytes);
  * "head_small" bf16 pyramid heads (Cout 4, C % 256 == 0): 1 (default) the wave-per-8-pixels head (GroupNorm fused)
  *   where the tiled head cannot take the image (H % 8 or W % 32 != 0), 2 also for up to 16384 output pixels, 0 never;
  * "head_part" tiled bf16 pyramid head with Cout 4: 1 (default) the halo's 36 tap partials as one 1x1 GEMM then their
- *   shifted sum (last_kernel 15), 0 nine tap GEMMs over the halo (last_kernel 10). */
+ *   shifted sum (last_kernel 15), 0 nine tap GEMMs over the halo (last_kernel 10);
+ * "gn_slice" snrse_gn_apply with statistics (no resampling): 1 (default) each block owns a 64-channel slice of its
+ *   pixels and folds only that slice's statistics, 0 each block folds all channels (equal results; read from the
+ *   process default context, as snrse_gn_apply takes none). */
 int snrse_set_option(const char* name, int value);
 
 /* Read back a switch (any name above) or: "halo_kernel" = generation of the halo conv kernel the current

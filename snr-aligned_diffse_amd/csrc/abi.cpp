@@ -62,6 +62,7 @@ int* option_field(snrse_ctx& c, const char* name) {
   if (name_is(name, "x3_tw")) return &c.x3_tw;
   if (name_is(name, "head_small")) return &c.head_small;
   if (name_is(name, "head_part")) return &c.head_part;
+  if (name_is(name, "gn_slice")) return &c.gn_slice;
   return nullptr;
 }
 

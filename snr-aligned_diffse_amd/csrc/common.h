@@ -196,6 +196,8 @@ struct snrse_ctx {
                                // take the image (H % 8 or W % 32), 2 also for <= 16384 output pixels, 0 never
   int head_part = 1;           // tiled pyramid head, Cout 4 (bf16): 1 the halo's 36 tap partials as a 1x1 GEMM + shifted
                                // sum (conv_head_part_kernel), 0 nine tap GEMMs over the halo (conv_head_kernel)
+  int gn_slice = 1;            // small-image gn_apply with the statistics fold: 1 blocks own 64-channel slices (each
+                               // folds 1/(C/64) of the image's statistics), 0 every block folds all C channels
   int ic_lds = 3;              // bf16 input conv: 1 the workgroup's input rows staged in LDS (W <= 1024), 2 the same
                                // with the channels split over wave pairs (4 waves / SIMD), 3 the output staged
                                // through LDS for 1-KB contiguous stores, 0 streaming loads

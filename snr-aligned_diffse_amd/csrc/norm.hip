@@ -100,18 +100,23 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const Tin* src0, int C0, 
                                                        int H, int W, const double* sums,
                                                        const double* sums1, const float* gamma,
                                                        const float* beta, int groups,
-                                                       float eps, int act, Tout* out, int opix_per_blk) {
+                                                       float eps, int act, Tout* out, int opix_per_blk, int csl) {
   constexpr int V = VecT<Tin>::N;
   static_assert(VecT<Tin>::N == VecT<Tout>::N || sizeof(Tout) == 4, "vec");
   const int C = C0 + C1;
   const int b = blockIdx.y;
   const int tid = threadIdx.x;
+  // csl > 0 (MODE_NONE, same-size output): this block owns channels [cs0, cs0 + csl) -- whole GroupNorm groups
+  // inside one source -- of its pixel range, so it folds only their statistics (blockIdx.x = range * nsl + slice)
+  const int nsl = csl > 0 ? C / csl : 1;
+  const int cs0 = csl > 0 ? (blockIdx.x % nsl) * csl : 0, cs1 = csl > 0 ? cs0 + csl : C;
+  const int bx = csl > 0 ? blockIdx.x / nsl : blockIdx.x;
   extern __shared__ __attribute__((aligned(16))) double gap_red[];  // [C][2] folded channel sums, then scale / shift
   double* const red = gap_red;
   float* const sc = (float*)(red + 2 * C);                         // scale[C], shift[C]
   if (sums) {
     // per channel: the SNRSE_STAT_SLOTS partial sums (independent 16-B loads), then per group from LDS
-    for (int c = tid; c < C; c += 256) {
+    for (int c = cs0 + tid; c < cs1; c += 256) {
       const double* st = c < C0 ? sums + stat_idx(b, 0, c, C0) : sums1 + stat_idx(b, 0, c - C0, C1);
       const size_t sstride = 2 * (size_t)(c < C0 ? C0 : C1);
       double s = 0.0, ss = 0.0;
@@ -126,7 +131,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const Tin* src0, int C0, 
     __syncthreads();
     const int cg = C / groups;
     const double cnt = (double)cg * H * W;
-    for (int c = tid; c < C; c += 256) {
+    for (int c = cs0 + tid; c < cs1; c += 256) {
       const int g = c / cg;
       double s = 0.0, ss = 0.0;
       for (int k = g * cg; k < (g + 1) * cg; ++k) {
@@ -149,20 +154,21 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const Tin* src0, int C0, 
   const int Wo = MODE == MODE_DOWN ? W / 2 : (MODE == MODE_UP ? 2 * W : W);
   const int LP = C / V;
   const int total = opix_per_blk * LP;
-  const int op0 = blockIdx.x * opix_per_blk;
+  const int op0 = bx * opix_per_blk;
   if constexpr (MODE == MODE_NONE && sizeof(Tout) == sizeof(Tin)) {
     // elementwise: UNR vectors' loads in flight before any is transformed (a load-use chain per vector held
     // the small-level GroupNorm launches at ~13 us); 16-bit takes the fast SiLU as gn_act does, fp32 the exact one
     constexpr int UNR = 4;
     const int HWo = Ho * Wo;
-    const int tot = min(opix_per_blk, HWo - op0) * LP;
+    const int LS = (cs1 - cs0) / V;  // vectors per pixel in this block's slice
+    const int tot = min(opix_per_blk, HWo - op0) * LS;
     for (int base = tid; base < tot; base += 256 * UNR) {
       u32x4 raw[UNR];
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const int idx = base + 256 * u;
         if (idx < tot) {
-          const int op = op0 + idx / LP, c = (idx % LP) * V;
+          const int op = op0 + idx / LS, c = cs0 + (idx % LS) * V;
           raw[u] = *(const u32x4*)(c < C0 ? src0 + ((size_t)b * HWo + op) * C0 + c
                                           : src1 + ((size_t)b * HWo + op) * C1 + (c - C0));
         }
@@ -171,7 +177,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const Tin* src0, int C0, 
       for (int u = 0; u < UNR; ++u) {
         const int idx = base + 256 * u;
         if (idx < tot) {
-          const int op = op0 + idx / LP, c = (idx % LP) * V;
+          const int op = op0 + idx / LS, c = cs0 + (idx % LS) * V;
           float x[V];
           if constexpr (sizeof(Tin) == 2) {
             unpack8<Tin>(raw[u], x);
@@ -361,6 +367,7 @@ template <typename Tin, typename Tout>
 static int launch_apply(const void* src0, int C0, const void* src1, int C1, int B, int H, int W,
                         const double* sums, const double* sums1, const float* gamma, const float* beta, int groups, float eps,
                         int act, int mode, void* out, hipStream_t stream) {
+  const bool slice = snrse_ctx_resolve(nullptr)->gn_slice != 0;  // (the process default context's switch)
   const int C = C0 + C1;
   const int Ho = mode == MODE_DOWN ? H / 2 : (mode == MODE_UP ? 2 * H : H);
   const int Wo = mode == MODE_DOWN ? W / 2 : (mode == MODE_UP ? 2 * W : W);
@@ -373,11 +380,24 @@ static int launch_apply(const void* src0, int C0, const void* src1, int C1, int 
   int opb = 256 / LP;
   if (opb < 1) opb = 1;
   if (sums) opb = std::max(opb, std::min((Ho * Wo + 15) / 16, 16 * 256 / LP));  // <= 16 folds per image, 16 vectors per thread
-  dim3 grid((Ho * Wo + opb - 1) / opb, B);
+  int nblk = (Ho * Wo + opb - 1) / opb, csl = 0;
+  // the same blocks as 64-channel slices x pixel ranges where a slice holds whole groups of one source: each
+  // block folds C / 64 times fewer statistics (16 slots x 16 B per channel, 64 KB per block at C = 256 -- the
+  // fold, not the image, was the small-level launch's traffic)
+  constexpr int kSl = 64;
+  if (slice && sums && mode == MODE_NONE && C > kSl && C % kSl == 0 && C0 % kSl == 0 && (C / groups) <= kSl &&
+      kSl % (C / groups) == 0) {
+    const int nsl = C / kSl;
+    const int npr = std::max(1, nblk / nsl);
+    opb = (Ho * Wo + npr - 1) / npr;
+    nblk = ((Ho * Wo + opb - 1) / opb) * nsl;
+    csl = kSl;
+  }
+  dim3 grid(nblk, B);
   const size_t lds = sizeof(double) * 2 * C + sizeof(float) * 2 * C;
 #define SNRSE_APPLY(MODE_)                                                                          \
   hipLaunchKernelGGL((gn_apply_kernel<Tin, Tout, MODE_>), grid, dim3(256), lds, stream, (const Tin*)src0, \
-                     C0, (const Tin*)src1, C1, H, W, sums, sums1, gamma, beta, groups, eps, act, (Tout*)out, opb)
+                     C0, (const Tin*)src1, C1, H, W, sums, sums1, gamma, beta, groups, eps, act, (Tout*)out, opb, csl)
   if (mode == MODE_NONE) SNRSE_APPLY(MODE_NONE);
   else if (mode == MODE_DOWN) SNRSE_APPLY(MODE_DOWN);
   else if (mode == MODE_UP) SNRSE_APPLY(MODE_UP);

@@ -141,7 +141,7 @@ def test_conv_small_cout_pyramid(gpu, dt):
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16", "fp16"])
-@pytest.mark.parametrize("HW", [(16, 32), (4, 8), (16, 64), (3, 5)])
+@pytest.mark.parametrize("HW", [(16, 32), (4, 8), (16, 64), (3, 5), (8, 16)])
 def test_gn_apply_small_image_single_launch(gpu, dt, HW):
     """GroupNorm(+SiLU) apply on both sides of ops.GN_FUSED_MAX_HW (512 px): one launch that folds the slotted
     statistics per block (the 16 x 32 .. 4 x 8 levels, ragged 3 x 5) and the gn_scale_shift + gn_act pair above
@@ -158,8 +158,16 @@ def test_gn_apply_small_image_single_launch(gpu, dt, HW):
     ref = F.silu(F.group_norm(x.double(), 32, g.double(), be.double(), eps=1e-6))
     xg = nhwc(x).to(gpu, dtype)
     s0, s1 = xg[..., :C0].contiguous(), xg[..., C0:].contiguous()
-    out = ops.gn_apply(s0, s1, ops.gn_stats(s0, s1), g.to(gpu), be.to(gpu), act=True)
+    sums = ops.gn_stats(s0, s1)
+    out = ops.gn_apply(s0, s1, sums, g.to(gpu), be.to(gpu), act=True)
     assert rel(nchw(out.float()), ref) < tol
+    # 64-channel slices per block (gn_slice 1, the default) and whole-C blocks give the same bits
+    ops.set_option("gn_slice", 0)
+    try:
+        whole = ops.gn_apply(s0, s1, sums, g.to(gpu), be.to(gpu), act=True)
+    finally:
+        ops.set_option("gn_slice", 1)
+    assert torch.equal(whole, out)
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16", "fp16"])
