@@ -1577,12 +1577,6 @@ __global__ __launch_bounds__(256) void conv_splitk_finalize(ConvParams p, int pp
 // like a halo, whose HBM latency then had one tap of cover each: 3-6 % slower on every shortcut shape, +0.9 % on the
 // C2 line, profiles/r05b_h5_sc_*.)  SCD = the launch has a shortcut; without one the loop is the 3-phase chunk loop.
 // T: the 16-bit input / weight format (bf16_t or f16_t), TO: the output type
-#ifndef SNRSE_H5_PX2
-#define SNRSE_H5_PX2 0
-#endif
-#ifndef SNRSE_H5_PX2_TAP
-#define SNRSE_H5_PX2_TAP 1
-#endif
 template <typename T, typename TO, int GNM, int EF, int TW, bool SCD>
 __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   constexpr int TH = 256 / TW, HC = TW + 2;
@@ -1594,7 +1588,6 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
   constexpr int SLOT = 3 * TAPB;
   constexpr int KT = 32;
   static_assert(64 * HJ >= HROWS, "halo rows");
-  constexpr bool PX2 = SNRSE_H5_PX2 && GNM > 0 && TW == 32 && !SCD;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const halo = smem;
   char* const ring = smem + HALO_BYTES;
@@ -1855,130 +1848,6 @@ __global__ __launch_bounds__(256, 2) void conv_halo5_kernel(ConvParams p) {
       }
       c = c2; pos = pos2; k = k2; ub = ub2;
     }
-  } else if constexpr (PX2) {
-  // PX2 (no shortcut, GroupNorm prologue, 8 x 32 tiles): the next chunk's halo is fetched and transformed a third per
-  // phase -- every phase loads one pair of this thread's 6 halo vectors of chunk c+1 (for the next phase) and
-  // transforms the pair loaded by the previous one beside its first tap's MFMAs, into a 6-vector register queue T
-  // shifted by one pair per phase -- so all phases run the same code (one MFMA body) and the chunk boundary holds only
-  // the LDS writes of T.  The affine of chunk c+1 is published by wave 0 at every phase top into one of two LDS
-  // slots (gnl + 64 (c+1 & 1)): three identical writes per chunk.
-  static_assert(HJ == 6, "PX2: 3 pairs of halo vectors per thread");
-  u32x4 Tq[6], R[2];
-  auto pair_pix = [&](int tp, int k, bool& ok) {  // (pixel, inside the image) of vector 2 tp + k, recomputed: a
-    // run-time index into hpix / hok would put them on the stack
-    const int hr = (tid >> 2) + 64 * (2 * tp + k);
-    const int hy = hr / HC, hx = hr - (hr / HC) * HC;
-    const int ih = h0 + hy - 1, iw = w0 + hx - 1;
-    ok = hr < HROWS && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W;
-    return (bb * p.H + ih) * p.W + iw;
-  };
-  auto pair_load = [&](int cc, int tp) {  // R <- raw vectors 2 tp, 2 tp + 1 of chunk cc (zeros past the last chunk)
-    const bool valid = cc < cbm;
-    const int ch = (valid ? cc : cbm - 1) * KT;
-    const bool s1 = ch >= p.C0;
-    const __amdgpu_buffer_rsrc_t r_ = make_rsrc(s1 ? p.src1 : p.src0, s1 ? p.bytes1 : p.bytes0);
-    const int cs_ = s1 ? p.C1 : p.C0, cc_ = (s1 ? ch - p.C0 : ch) + hcol * 8;
-    // the affine first: a phase top waits for it (and the weights) while the pair stays in flight (vmcnt(2))
-    if (tid < 16) gnv = *(const f32x4*)((tid < 8 ? p.gn_scale : p.gn_shift) + (size_t)bb * Cin + ch + (tid & 7) * 4);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      bool ok;
-      const int pix = pair_pix(tp, k, ok);
-      R[k] = __builtin_amdgcn_raw_buffer_load_b128(r_, (ok && valid) ? (pix * cs_ + cc_) * 2 : (int)0x80000000, 0, 0);
-    }
-  };
-  auto gn_publish_to = [&](int slot) {
-    if (tid < 16) {
-      f32x4 g = gnv;
-      if constexpr (GNM == 2) g *= kNegLog2e;
-      *(f32x4*)(gnl + 64 * slot + tid * 4) = g;
-    }
-  };
-  auto affine_from = [&](int slot, float* gsc, float* gsh) {
-    const float* gb = gnl + 64 * slot;
-    const f32x4 s0 = *(const f32x4*)(gb + hcol * 8), s1 = *(const f32x4*)(gb + hcol * 8 + 4);
-    const f32x4 t0 = *(const f32x4*)(gb + 32 + hcol * 8), t1 = *(const f32x4*)(gb + 32 + hcol * 8 + 4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { gsc[i] = s0[i]; gsc[4 + i] = s1[i]; gsh[i] = t0[i]; gsh[4 + i] = t1[i]; }
-  };
-  // prologue: chunk 0's whole halo through Tq, then chunk 1's first pair in flight
-  {
-    const __amdgpu_buffer_rsrc_t r_ = make_rsrc(p.src0, p.bytes0);
-#pragma unroll
-    for (int j = 0; j < 6; ++j)
-      Tq[j] = __builtin_amdgcn_raw_buffer_load_b128(r_, hok[j] ? (hpix[j] * p.C0 + hcol * 8) * 2 : (int)0x80000000, 0, 0);
-    if (tid < 16) gnv = *(const f32x4*)((tid < 8 ? p.gn_scale : p.gn_shift) + (size_t)bb * Cin + (tid & 7) * 4);
-  }
-  dma(0, 0, 0, ring);
-  gn_publish_to(0);
-  __syncthreads();
-  {
-    float gsc[8], gsh[8];
-    affine_from(0, gsc, gsh);
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int hr = (tid >> 2) + 64 * j;
-      if (j == 5 && hr >= HROWS) break;
-      *(u32x4*)(halo + swz64(hr, hcol)) = gn_xform8<T, GNM>(Tq[j], gsc, gsh, hok[j]);
-    }
-  }
-  pair_load(1, 0);
-  SNRSE_STAMP(1);
-  for (int q = 0; q < nq; ++q) {
-    const int c = q / 3, tq = q - c * 3, t0 = tq * 3;
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // this phase's weights and wave 0's affine; the pair may fly
-    gn_publish_to((c + 1) & 1);  // chunk c+1's affine (loaded with the pair this phase transforms)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    SNRSE_STAMP(2 + 2 * (q & 15));
-    dma(q + 1 < nq ? (q + 1) / 3 : 0, (q + 1) % 3, 0, ring + ((q + 1) & 1) * SLOT, q + 1 >= nq);
-    float gsc[8], gsh[8];
-    affine_from((c + 1) & 1, gsc, gsh);
-    const char* sl = ring + (q & 1) * SLOT;
-#pragma unroll
-    for (int jt = 0; jt < 3; ++jt) {
-      const int tp = t0 + jt;
-      const int dy = tp / 3 - 1, dx = tp - (tp / 3) * 3 - 1;
-      const int hbase = (wid * RW + dy + 1) * HC + dx + 1 + lrow;
-      const char* sb = sl + jt * TAPB;
-      u32x4 af[4], bfr[8];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = *(const u32x4*)(halo + swz64(hbase + (16 * i / TW) * HC + (16 * i) % TW, lg));
-#pragma unroll
-      for (int j = 0; j < 8; ++j) bfr[j] = *(const u32x4*)(sb + swz64(j * 16 + lrow, lg));
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[h][i][j] = mfma_chunk<T>(af[i], bfr[h * 4 + j], acc[h][i][j]);  // D[px][co]
-      if (jt == SNRSE_H5_PX2_TAP) {
-        // this phase's pair (vectors 2 tq, 2 tq + 1 of chunk c+1) after this tap's MFMAs, then the next phase's loads;
-        // the builtin wait (visible to the compiler's model) lets only this phase's 6 weight pieces stay in flight
-        __builtin_amdgcn_s_waitcnt(0x0f76);  // vmcnt(6)
-        bool ok0, ok1;
-        (void)pair_pix(tq, 0, ok0);
-        (void)pair_pix(tq, 1, ok1);
-        const u32x4 x0 = gn_xform8<T, GNM, false>(R[0], gsc, gsh, ok0);
-        const u32x4 x1 = gn_xform8<T, GNM, false>(R[1], gsc, gsh, ok1);
-        Tq[0] = Tq[2]; Tq[1] = Tq[3]; Tq[2] = Tq[4]; Tq[3] = Tq[5]; Tq[4] = x0; Tq[5] = x1;
-        const int qn = q + 1, cn = qn / 3;
-        pair_load(cn + 1, qn - cn * 3);
-      }
-    }
-    SNRSE_STAMP(3 + 2 * (q & 15));
-    if (tq == 2 && c + 1 < cbm) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // every wave is done reading halo(c)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const int hr = (tid >> 2) + 64 * j;
-        if (j == 5 && hr >= HROWS) break;
-        *(u32x4*)(halo + swz64(hr, hcol)) = Tq[j];
-      }
-    }
-  }
   } else {
   // no shortcut: 3 phases of 3 taps per chunk, the next chunk's halo stored behind one more barrier
   halo_load(0);

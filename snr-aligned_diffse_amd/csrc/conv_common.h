@@ -141,9 +141,7 @@ SNRSE_DEV int swz64(int row, int chunk) { return (row << 6) + ((chunk ^ ((row >>
 // (fma, exp, fma, rcp, mul) instead of 6.  z -> +inf gives -0 (SiLU's limit), z -> -inf gives y.
 SNRSE_DEV float gn_silu_prescale(float v) { return v * kNegLog2e; }  // (kNegLog2e: common.h)
 
-// SB = false: no scheduling barriers between the stages (a caller that places the transform beside MFMAs, whose
-// issue gaps cover the exp / rcp latencies)
-template <typename T, int GNM, bool SB = true>
+template <typename T, int GNM>
 SNRSE_DEV u32x4 gn_xform8(const u32x4 v, const float* sc, const float* sh, bool ok) {
   float y[8];
 #pragma unroll
@@ -157,10 +155,10 @@ SNRSE_DEV u32x4 gn_xform8(const u32x4 v, const float* sc, const float* sh, bool 
     float e[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_exp2f(y[k]);
-    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < 8; ++k) e[k] = __builtin_amdgcn_rcpf(fmaf(e[k], kNegInvLn2, kNegInvLn2));
-    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < 8; ++k) y[k] *= e[k];
   }
