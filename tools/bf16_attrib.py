@@ -15,7 +15,7 @@ point where the HIP bf16 path (snrse/ncsnpp.py) holds a tensor in 16 bits.  Each
 Every class is rounded to `fmt[class]` in {"bf16", "fp16", "fp32"} (fp32 = not rounded).  Runs the reference's
 one-NFE golden (ncsnpp_full.npz) and its N = 5 OUVE PC golden (pc_ouve.npz, 10 NFE with the recorded draws) and
 prints relative / absolute RMS against them, plus the largest magnitude every class held (fp16 range check).
-Usage: python tools/bf16_attrib.py [preset ...]   (presets below; default: all).
+Usage: [EMU_SD=state_dict] python tools/bf16_attrib.py [preset ...]   (presets below; default: all).
 Test infrastructure: reads oracle/ and tests/golden; nothing on the product path imports it."""
 import json
 import math
@@ -150,11 +150,25 @@ _SD = None
 
 
 def weights():
+    """The formula weights, or EMU_SD=path: an NCSN++ state dict (.safetensors, or a torch file read with
+    weights_only=True; a Lightning checkpoint's 'state_dict' with its 'dnn.' prefix is accepted) -- the maxabs
+    columns then say how far that checkpoint's activations sit from the 16-bit formats' ranges."""
     global _SD
     if _SD is None:
-        with open(os.path.join(ROOT, "tests", "golden", "state_dict_keys.json")) as f:
-            shapes = {k: tuple(s) for k, s in json.load(f)["ncsnpp"]}
-        _SD = state_dict_to_torch(formula.formula_state_dict(shapes))
+        path = os.environ.get("EMU_SD")
+        if path:
+            if path.endswith(".safetensors"):
+                from safetensors.torch import load_file
+                sd = load_file(path)
+            else:
+                sd = torch.load(path, map_location="cpu", weights_only=True)
+                sd = sd.get("state_dict", sd)
+            sd = {k[4:] if k.startswith("dnn.") else k: v for k, v in sd.items()}
+            _SD = state_dict_to_torch({k: v.float().numpy() for k, v in sd.items() if torch.is_tensor(v)})
+        else:
+            with open(os.path.join(ROOT, "tests", "golden", "state_dict_keys.json")) as f:
+                shapes = {k: tuple(s) for k, s in json.load(f)["ncsnpp"]}
+            _SD = state_dict_to_torch(formula.formula_state_dict(shapes))
     return _SD
 
 
